@@ -1,0 +1,139 @@
+/*
+ * nrx.h -- C ABI of the MI355X CGNN neural-receiver engine (libnrx.so).
+ *
+ * Plain C, plain pointers and sizes: no torch, no HIP types in the signatures
+ * (streams are passed as `void*` = hipStream_t).  Every entry point returns an int
+ * status (NRX_OK = 0, negative on error) and never throws; the last error message of
+ * the calling thread is available from nrx_last_error().
+ *
+ * The reference has no FFI for this path: its hot path is a Python layer call,
+ *   CGNN.forward([y, pe, h_hat, active_tx, mcs_ue_mask]) -> (llrs, h_hats)
+ *       (utils/neural_rx.py:544-595; faithful TF structure in
+ *        utils/neural_rx copy_pytorch.py:474-514),
+ * wrapped by CGNNOFDM.forward (neural_rx.py:813-881) and
+ * NeuralReceiverONNX.forward (neural_rx.py:1773-1812).  The entry points below are
+ * what a binding of that call needs; INTEGRATION.md shows the
+ * ctypes binding the Python layer uses.
+ *
+ * Layouts (all channels-last, as the reference's NHWC tensors):
+ *   y        [B][F][T][2A]          f32  channels [Re a0..a(A-1), Im a0..a(A-1)]
+ *   pe       [U][F][T][2]           f32  [time, freq] nearest-pilot encoding
+ *   h_hat    [B][U][F][T][2A]       f32  initial channel estimate (NULL if unused)
+ *   active   [B][U]                 f32  1 = DMRS port active
+ *   mcs_mask [B][U][M]              f32  Var-IO state-init mixing weights (NULL: one-hot m=0)
+ *   llr      [H][B][U][F][T][bits_max] f32 out, H = number of LLR heads
+ *                                   (M for Var-IO, 1 otherwise); head h fills its
+ *                                   first bits_h entries, the rest are written 0
+ *   h_ref    [B][U][F][T][2A]       f32 out (NULL to skip the ChEst readout)
+ * Sign convention: Sionna's LLR = log p(b=1)/p(b=0) (the Aerial layout negates,
+ * neural_rx.py:1811; the Python layer does that, not the kernels).
+ */
+#ifndef NRX_H_
+#define NRX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NRX_API_VERSION 1
+
+enum nrx_status {
+  NRX_OK = 0,
+  NRX_ERR_INVALID_ARG = -1,   /* null pointer / bad enum / bad num_it */
+  NRX_ERR_SHAPE = -2,         /* shape inconsistent with the model or limits */
+  NRX_ERR_UNSUPPORTED = -3,   /* topology the kernels are not built for */
+  NRX_ERR_HIP = -4,           /* HIP runtime error (message has the HIP string) */
+  NRX_ERR_NOMEM = -5,
+  NRX_ERR_WORKSPACE = -6      /* workspace too small */
+};
+
+/* Arithmetic of a forward pass. */
+enum nrx_precision {
+  NRX_PREC_F16 = 0,    /* perf mode: f16 activations, f16 depthwise, f16 MFMA with f32
+                          accumulation (the reference's own TRT export ran --fp16) */
+  NRX_PREC_F32X = 1    /* parity mode: f32 activations, f64 arithmetic (f64 MFMA) */
+};
+
+/* Model topology.  Mirrors the [neural_receiver] block of the reference cfg
+ * (config/nrx_rt.cfg:57-75) plus [system] num_rx_antennas / mcs_index. */
+typedef struct nrx_desc {
+  int32_t num_rx_ant;        /* A (4 or 16) */
+  int32_t d_s;               /* state width; kernels are built for 56 */
+  int32_t num_it;            /* trained CGNN iterations (len(iterations)) */
+  int32_t num_mcs;           /* M = len(mcs_index), 1..8 */
+  int32_t bits[8];           /* bits per symbol of each MCS (2, 4 or 6) */
+  int32_t var_mcs_masking;   /* 1: one StateInit + one LLR head of max(bits), sliced */
+  int32_t init_units[2];     /* num_units_init, kernels built for {128,128} */
+  int32_t agg_units;         /* num_units_agg[i] = [64] */
+  int32_t state_units[2];    /* num_units_state[i] = [128,128] */
+  int32_t readout_units;     /* num_units_readout = [128] */
+  int32_t use_h_hat;         /* 1: StateInit consumes h_hat (initial_chest = "ls") */
+} nrx_desc;
+
+typedef struct nrx_shape {
+  int32_t batch;             /* B slots */
+  int32_t num_tx;            /* U users (DMRS ports) */
+  int32_t num_subcarriers;   /* F = 12 * PRBs */
+  int32_t num_symbols;       /* T, must be 14 */
+} nrx_shape;
+
+typedef struct nrx_io {
+  nrx_shape shape;
+  int32_t num_it;            /* iterations to run, 1..desc.num_it (CGNN.num_it setter) */
+  int32_t precision;         /* enum nrx_precision */
+  const float* y;
+  const float* pe;
+  const float* h_hat;        /* may be NULL only if desc.use_h_hat == 0 */
+  const float* active;
+  const float* mcs_mask;     /* may be NULL: treated as one-hot on MCS 0 */
+  float* llr;
+  float* h_ref;              /* may be NULL */
+} nrx_io;
+
+typedef struct nrx_handle nrx_handle;
+
+/* Create an engine on `device` from weights in Keras get_weights() order
+ * (the reference loads the same list with
+ * utils/utils.py:53-70 load_weights).  `weight_sizes[i]` is the element count of
+ * weights[i] and is validated against the topology.  Weights are host pointers;
+ * they are copied, converted and packed into device buffers. */
+int nrx_create(const nrx_desc* desc, const float* const* weights, const int64_t* weight_sizes,
+               int32_t num_weights, int32_t device, nrx_handle** out);
+
+/* Number of weight arrays and the element count of array i for a topology. */
+int nrx_weight_layout(const nrx_desc* desc, int32_t* num_weights, int64_t* sizes, int32_t cap);
+
+/* Device workspace (bytes) a forward of this shape/precision needs. */
+int nrx_workspace_size(const nrx_handle* h, const nrx_shape* shape, int32_t precision,
+                       size_t* bytes);
+
+/* Asynchronous forward on `stream` (hipStream_t; NULL = default stream).
+ * All pointers in `io` and `workspace` are device pointers.  No allocation, no host
+ * synchronisation: the call can be captured into a hipGraph. */
+int nrx_forward(nrx_handle* h, const nrx_io* io, void* workspace, size_t workspace_bytes,
+                void* stream);
+
+void nrx_destroy(nrx_handle* h);
+
+/* Host helper: nearest-pilot positional encoding pe[U][F][T][2] for DMRS
+ * configuration type 1 (restates onnx_utils.py:172-260 for the product path).
+ * dmrs_symbols: the DMRS OFDM symbol indices; cdm_group[u] in {0,1}. */
+int nrx_compute_pe(int32_t num_tx, int32_t num_subcarriers, int32_t num_symbols,
+                   const int32_t* dmrs_symbols, int32_t num_dmrs_symbols,
+                   const int32_t* cdm_group, float* pe_out);
+
+/* Algorithmic FLOPs of one forward per resource element per user
+ * (SURVEY.md 8(d) formula). */
+double nrx_flops_per_re_user(const nrx_desc* desc, int32_t num_it);
+
+const char* nrx_last_error(void);
+int32_t nrx_api_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NRX_H_ */

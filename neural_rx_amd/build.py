@@ -1,0 +1,52 @@
+"""Build ``libnrx.so`` in-tree with hipcc for gfx950.
+
+    python -m neural_rx_amd.build [--force]
+
+The library is written to ``neural_rx_amd/lib/libnrx.so`` (git-ignored, but it
+travels to the GPU box with the repository snapshot).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "lib", "libnrx.so")
+SOURCES = [os.path.join(CSRC, "nrx_kernels.hip"), os.path.join(CSRC, "nrx_api.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, "nrx_internal.h"),
+                  os.path.join(HERE, "..", "include", "nrx.h")]
+ARCH = os.environ.get("NRX_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.sep not in c or os.path.exists(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(d) > t for d in DEPS if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and not needs_build():
+        return LIB
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    tmp = LIB + f".tmp{os.getpid()}"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-function", *SOURCES, "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,457 @@
+// nrx_api.cpp -- host side of libnrx.so: C ABI (include/nrx.h), weight validation and
+// packing, workspace sizing, forward dispatch, and the product-side positional encoding.
+//
+// Weight order = Keras get_weights() of the reference CGNN:
+//   StateInit x num_init : 3 x (dw[3,3,Cin,1], pw[1,1,Cin,Cout], b[Cout])
+//   num_it x [ Agg: (W[ds,64], b), (W[64,ds], b) ; Update: 3 x sep ]
+//   LLR heads x H : (W[ds,128], b), (W[128,bits], b)
+//   ChEst : (W[ds,128], b), (W[128,2A], b)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/nrx.h"
+#include "nrx_internal.h"
+
+namespace nrx {
+hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args,
+                              const ModelW<_Float16, float>& W, int num_it, hipStream_t st);
+hipError_t launch_forward_f64(const FwdArgs<double, double, float>& args,
+                              const ModelW<double, double>& W, int num_it, hipStream_t st);
+hipError_t setup_kernels();
+int strip_width(int precision);
+}  // namespace nrx
+
+using namespace nrx;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(NRX_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct LayerShape {
+  enum Kind { SEP, DENSE } kind;
+  int cin, cout;
+};
+
+// Topology checks: the kernels are specialised for the in-scope configs.
+int check_desc(const nrx_desc* d) {
+  if (!d) return fail(NRX_ERR_INVALID_ARG, "desc is NULL");
+  if (d->d_s != kDS) return fail(NRX_ERR_UNSUPPORTED, "kernels are built for d_s = 56");
+  if (d->init_units[0] != kHID || d->init_units[1] != kHID || d->state_units[0] != kHID ||
+      d->state_units[1] != kHID || d->readout_units != kHID || d->agg_units != kAGG)
+    return fail(NRX_ERR_UNSUPPORTED, "kernels are built for 128/128 convs, 64 agg, 128 readout");
+  if (d->num_rx_ant < 1 || 4 * d->num_rx_ant + 2 > 128 || 2 * d->num_rx_ant > 32)
+    return fail(NRX_ERR_UNSUPPORTED, "num_rx_ant must be 1..16");
+  if (d->num_it < 1 || d->num_it > kMaxIt) return fail(NRX_ERR_UNSUPPORTED, "num_it must be 1..8");
+  if (d->num_mcs < 1 || d->num_mcs > kMaxHeads) return fail(NRX_ERR_UNSUPPORTED, "num_mcs must be 1..8");
+  for (int m = 0; m < d->num_mcs; ++m)
+    if (d->bits[m] < 1 || d->bits[m] > 8) return fail(NRX_ERR_UNSUPPORTED, "bits must be 1..8");
+  if (d->use_h_hat != 0 && d->use_h_hat != 1) return fail(NRX_ERR_INVALID_ARG, "use_h_hat must be 0/1");
+  return NRX_OK;
+}
+
+int num_init(const nrx_desc* d) { return d->var_mcs_masking ? 1 : d->num_mcs; }
+int num_heads(const nrx_desc* d) { return d->var_mcs_masking ? 1 : d->num_mcs; }
+int bits_max(const nrx_desc* d) {
+  int b = 0;
+  for (int m = 0; m < d->num_mcs; ++m) b = d->bits[m] > b ? d->bits[m] : b;
+  return b;
+}
+int init_cin(const nrx_desc* d) { return (d->use_h_hat ? 4 : 2) * d->num_rx_ant + 2; }
+
+std::vector<LayerShape> layer_list(const nrx_desc* d) {
+  std::vector<LayerShape> L;
+  for (int m = 0; m < num_init(d); ++m) {
+    L.push_back({LayerShape::SEP, init_cin(d), kHID});
+    L.push_back({LayerShape::SEP, kHID, kHID});
+    L.push_back({LayerShape::SEP, kHID, kDS});
+  }
+  for (int i = 0; i < d->num_it; ++i) {
+    L.push_back({LayerShape::DENSE, kDS, kAGG});
+    L.push_back({LayerShape::DENSE, kAGG, kDS});
+    L.push_back({LayerShape::SEP, 2 * kDS + 2, kHID});
+    L.push_back({LayerShape::SEP, kHID, kHID});
+    L.push_back({LayerShape::SEP, kHID, kDS});
+  }
+  const int nh = num_heads(d);
+  for (int h = 0; h < nh; ++h) {
+    L.push_back({LayerShape::DENSE, kDS, kHID});
+    L.push_back({LayerShape::DENSE, kHID, d->var_mcs_masking ? bits_max(d) : d->bits[h]});
+  }
+  L.push_back({LayerShape::DENSE, kDS, kHID});
+  L.push_back({LayerShape::DENSE, kHID, 2 * d->num_rx_ant});
+  return L;
+}
+
+std::vector<int64_t> weight_sizes(const nrx_desc* d) {
+  std::vector<int64_t> s;
+  for (const auto& l : layer_list(d)) {
+    if (l.kind == LayerShape::SEP) {
+      s.push_back(9LL * l.cin);
+      s.push_back((int64_t)l.cin * l.cout);
+      s.push_back(l.cout);
+    } else {
+      s.push_back((int64_t)l.cin * l.cout);
+      s.push_back(l.cout);
+    }
+  }
+  return s;
+}
+
+int round_up(int x, int m) { return (x + m - 1) / m * m; }
+int pow2_at_least(int x, int lo) {
+  int p = lo;
+  while (p < x) p *= 2;
+  return p;
+}
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// Host-side packing into one contiguous blob per precision; pointers are patched to the
+// device copy after upload.
+template <class WT, class BT>
+struct Packer {
+  std::vector<char> blob;
+  size_t put_w(const std::vector<WT>& v) {
+    size_t off = align256(blob.size());
+    blob.resize(off + v.size() * sizeof(WT));
+    memcpy(blob.data() + off, v.data(), v.size() * sizeof(WT));
+    return off;
+  }
+  size_t put_b(const std::vector<BT>& v) {
+    size_t off = align256(blob.size());
+    blob.resize(off + v.size() * sizeof(BT));
+    memcpy(blob.data() + off, v.data(), v.size() * sizeof(BT));
+    return off;
+  }
+  // offsets relative to blob start, fixed up later
+  struct SepOff { size_t dw, pw, b; };
+  struct DenOff { size_t w, b; };
+  SepOff sep(const float* dw, const float* pw, const float* b, int cin, int cout, int cinp, int coutp) {
+    std::vector<WT> dwp((size_t)9 * cinp, WT(0)), pwp((size_t)coutp * cinp, WT(0));
+    std::vector<BT> bp(coutp, BT(0));
+    for (int tap = 0; tap < 9; ++tap)
+      for (int c = 0; c < cin; ++c) dwp[(size_t)tap * cinp + c] = (WT)dw[(size_t)tap * cin + c];
+    for (int c = 0; c < cin; ++c)
+      for (int o = 0; o < cout; ++o) pwp[(size_t)o * cinp + c] = (WT)pw[(size_t)c * cout + o];
+    for (int o = 0; o < cout; ++o) bp[o] = (BT)b[o];
+    SepOff r;
+    r.dw = put_w(dwp);
+    r.pw = put_w(pwp);
+    r.b = put_b(bp);
+    return r;
+  }
+  DenOff dense(const float* w, const float* b, int cin, int cout, int cinp, int coutp) {
+    std::vector<WT> wp((size_t)coutp * cinp, WT(0));
+    std::vector<BT> bp(coutp, BT(0));
+    for (int c = 0; c < cin; ++c)
+      for (int o = 0; o < cout; ++o) wp[(size_t)o * cinp + c] = (WT)w[(size_t)c * cout + o];
+    for (int o = 0; o < cout; ++o) bp[o] = (BT)b[o];
+    return DenOff{put_w(wp), put_b(bp)};
+  }
+};
+
+template <class WT, class BT>
+struct DeviceModel {
+  ModelW<WT, BT> W{};
+  void* dev = nullptr;
+  int init_cinp = 0;
+};
+
+template <class WT, class BT>
+int build_model(const nrx_desc* d, const float* const* w, int kc, DeviceModel<WT, BT>* out) {
+  Packer<WT, BT> pk;
+  using SO = typename Packer<WT, BT>::SepOff;
+  using DO = typename Packer<WT, BT>::DenOff;
+  SO init[kMaxInit][3];
+  DO agg[kMaxIt][2];
+  SO upd[kMaxIt][3];
+  DO llr[kMaxHeads][2];
+  DO ch[2];
+  const int icin = init_cin(d);
+  const int icinp = pow2_at_least(round_up(icin, kc), 32);
+  out->init_cinp = icinp;
+  int k = 0;
+  auto sep = [&](int cin, int cout, int cinp, int coutp) {
+    SO r = pk.sep(w[k], w[k + 1], w[k + 2], cin, cout, cinp, coutp);
+    k += 3;
+    return r;
+  };
+  auto den = [&](int cin, int cout, int cinp, int coutp) {
+    DO r = pk.dense(w[k], w[k + 1], cin, cout, cinp, coutp);
+    k += 2;
+    return r;
+  };
+  for (int m = 0; m < num_init(d); ++m) {
+    init[m][0] = sep(icin, kHID, icinp, kHID);
+    init[m][1] = sep(kHID, kHID, kHID, kHID);
+    init[m][2] = sep(kHID, kDS, kHID, kDSP);
+  }
+  for (int i = 0; i < d->num_it; ++i) {
+    agg[i][0] = den(kDS, kAGG, kDSP, kAGG);
+    agg[i][1] = den(kAGG, kDS, kAGG, kDSP);
+    upd[i][0] = sep(2 * kDS + 2, kHID, kUPD_CINP, kHID);
+    upd[i][1] = sep(kHID, kHID, kHID, kHID);
+    upd[i][2] = sep(kHID, kDS, kHID, kDSP);
+  }
+  for (int h = 0; h < num_heads(d); ++h) {
+    const int nb = d->var_mcs_masking ? bits_max(d) : d->bits[h];
+    llr[h][0] = den(kDS, kHID, kDSP, kHID);
+    llr[h][1] = den(kHID, nb, kHID, 16);
+  }
+  const int a2 = 2 * d->num_rx_ant;
+  ch[0] = den(kDS, kHID, kDSP, kHID);
+  ch[1] = den(kHID, a2, kHID, a2 <= 16 ? 16 : 32);
+
+  hipError_t e = hipMalloc(&out->dev, pk.blob.size());
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc(weights)");
+  e = hipMemcpy(out->dev, pk.blob.data(), pk.blob.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpy(weights)");
+  char* base = (char*)out->dev;
+  auto fs = [&](const SO& o) {
+    return SepW<WT, BT>{(const WT*)(base + o.dw), (const WT*)(base + o.pw), (const BT*)(base + o.b)};
+  };
+  auto fd = [&](const DO& o) { return DenseW<WT, BT>{(const WT*)(base + o.w), (const BT*)(base + o.b)}; };
+  for (int m = 0; m < num_init(d); ++m)
+    for (int l = 0; l < 3; ++l) out->W.init[m][l] = fs(init[m][l]);
+  for (int i = 0; i < d->num_it; ++i) {
+    out->W.agg[i][0] = fd(agg[i][0]);
+    out->W.agg[i][1] = fd(agg[i][1]);
+    for (int l = 0; l < 3; ++l) out->W.upd[i][l] = fs(upd[i][l]);
+  }
+  for (int h = 0; h < num_heads(d); ++h) {
+    out->W.llr[h][0] = fd(llr[h][0]);
+    out->W.llr[h][1] = fd(llr[h][1]);
+  }
+  out->W.chest[0] = fd(ch[0]);
+  out->W.chest[1] = fd(ch[1]);
+  return NRX_OK;
+}
+
+}  // namespace
+
+struct nrx_handle {
+  nrx_desc desc;
+  int device;
+  DeviceModel<_Float16, float> m16;
+  DeviceModel<double, double> m64;
+};
+
+static size_t state_bytes(const nrx_shape* s, int precision) {
+  const size_t es = precision == NRX_PREC_F16 ? 2 : 4;
+  return align256((size_t)s->batch * s->num_tx * s->num_subcarriers * kTP * kDSP * es);
+}
+
+static int check_shape(const nrx_shape* s) {
+  if (!s) return fail(NRX_ERR_INVALID_ARG, "shape is NULL");
+  if (s->num_symbols != kT) return fail(NRX_ERR_SHAPE, "num_symbols must be 14");
+  if (s->batch < 1 || s->batch > 65535) return fail(NRX_ERR_SHAPE, "batch must be 1..65535");
+  if (s->num_tx < 1 || s->num_tx > kMaxUsers) return fail(NRX_ERR_SHAPE, "num_tx must be 1..16");
+  if (s->num_subcarriers < 1 || s->num_subcarriers > 12 * 275)
+    return fail(NRX_ERR_SHAPE, "num_subcarriers must be 1..3300");
+  return NRX_OK;
+}
+
+template <class WT, class BT, class S>
+static void fill_args(FwdArgs<WT, BT, S>& a, const nrx_handle* h, const nrx_io* io, void* ws, int init_cinp) {
+  const nrx_desc* d = &h->desc;
+  const nrx_shape* s = &io->shape;
+  a.B = s->batch;
+  a.U = s->num_tx;
+  a.F = s->num_subcarriers;
+  a.A = d->num_rx_ant;
+  a.M = d->num_mcs;
+  a.H = num_heads(d);
+  a.init_cinp = init_cinp;
+  a.num_init = num_init(d);
+  a.masking = d->var_mcs_masking;
+  a.use_h = d->use_h_hat;
+  a.bits_max = bits_max(d);
+  for (int i = 0; i < kMaxHeads; ++i)
+    a.head_bits[i] = i < a.H ? (d->var_mcs_masking ? bits_max(d) : d->bits[i]) : 0;
+  a.y = io->y;
+  a.pe = io->pe;
+  a.h_hat = io->h_hat;
+  a.active = io->active;
+  a.mcs_mask = io->mcs_mask;
+  a.llr = io->llr;
+  a.h_ref = io->h_ref;
+  char* p = (char*)ws;
+  a.norm = (double*)p;
+  p += align256((size_t)s->batch * sizeof(double));
+  const size_t sb = state_bytes(s, io->precision);
+  a.s_in = (S*)(p + sb);
+  a.s_out = (S*)p;
+  a.a = (S*)(p + 2 * sb);
+}
+
+
+extern "C" {
+
+const char* nrx_last_error(void) { return g_err.c_str(); }
+int32_t nrx_api_version(void) { return NRX_API_VERSION; }
+
+int nrx_weight_layout(const nrx_desc* desc, int32_t* num_weights, int64_t* sizes, int32_t cap) {
+  int rc = check_desc(desc);
+  if (rc) return rc;
+  if (!num_weights) return fail(NRX_ERR_INVALID_ARG, "num_weights is NULL");
+  std::vector<int64_t> s = weight_sizes(desc);
+  *num_weights = (int32_t)s.size();
+  if (sizes)
+    for (int i = 0; i < (int)s.size() && i < cap; ++i) sizes[i] = s[i];
+  return NRX_OK;
+}
+
+int nrx_create(const nrx_desc* desc, const float* const* weights, const int64_t* sizes,
+               int32_t num_weights, int32_t device, nrx_handle** out) {
+  int rc = check_desc(desc);
+  if (rc) return rc;
+  if (!weights || !sizes || !out) return fail(NRX_ERR_INVALID_ARG, "null argument");
+  std::vector<int64_t> exp = weight_sizes(desc);
+  if ((int)exp.size() != num_weights)
+    return fail(NRX_ERR_SHAPE, "expected " + std::to_string(exp.size()) + " weight arrays, got " +
+                                   std::to_string(num_weights));
+  for (int i = 0; i < num_weights; ++i) {
+    if (!weights[i]) return fail(NRX_ERR_INVALID_ARG, "weight " + std::to_string(i) + " is NULL");
+    if (sizes[i] != exp[i])
+      return fail(NRX_ERR_SHAPE, "weight " + std::to_string(i) + " has " + std::to_string(sizes[i]) +
+                                     " elements, expected " + std::to_string(exp[i]));
+  }
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  e = setup_kernels();
+  if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute");
+  nrx_handle* h = new nrx_handle();
+  h->desc = *desc;
+  h->device = device;
+  rc = build_model<_Float16, float>(desc, weights, 32, &h->m16);
+  if (!rc) rc = build_model<double, double>(desc, weights, 16, &h->m64);
+  if (rc) {
+    nrx_destroy(h);
+    return rc;
+  }
+  *out = h;
+  return NRX_OK;
+}
+
+void nrx_destroy(nrx_handle* h) {
+  if (!h) return;
+  if (h->m16.dev) (void)hipFree(h->m16.dev);
+  if (h->m64.dev) (void)hipFree(h->m64.dev);
+  delete h;
+}
+
+int nrx_workspace_size(const nrx_handle* h, const nrx_shape* shape, int32_t precision, size_t* bytes) {
+  if (!h || !bytes) return fail(NRX_ERR_INVALID_ARG, "null argument");
+  int rc = check_shape(shape);
+  if (rc) return rc;
+  if (precision != NRX_PREC_F16 && precision != NRX_PREC_F32X)
+    return fail(NRX_ERR_INVALID_ARG, "unknown precision");
+  *bytes = align256((size_t)shape->batch * sizeof(double)) + 3 * state_bytes(shape, precision);
+  return NRX_OK;
+}
+
+int nrx_forward(nrx_handle* h, const nrx_io* io, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!h || !io) return fail(NRX_ERR_INVALID_ARG, "null argument");
+  int rc = check_shape(&io->shape);
+  if (rc) return rc;
+  const nrx_desc* d = &h->desc;
+  if (io->num_it < 1 || io->num_it > d->num_it) return fail(NRX_ERR_INVALID_ARG, "Invalid number of iterations");
+  if (!io->y || !io->pe || !io->active || !io->llr) return fail(NRX_ERR_INVALID_ARG, "null tensor pointer");
+  if (d->use_h_hat && !io->h_hat) return fail(NRX_ERR_INVALID_ARG, "h_hat is required by this model");
+  size_t need = 0;
+  rc = nrx_workspace_size(h, &io->shape, io->precision, &need);
+  if (rc) return rc;
+  if (!workspace || workspace_bytes < need)
+    return fail(NRX_ERR_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes");
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e;
+  if (io->precision == NRX_PREC_F16) {
+    FwdArgs<_Float16, float, _Float16> a{};
+    fill_args(a, h, io, workspace, h->m16.init_cinp);
+    e = launch_forward_f16(a, h->m16.W, io->num_it, st);
+  } else {
+    FwdArgs<double, double, float> a{};
+    fill_args(a, h, io, workspace, h->m64.init_cinp);
+    e = launch_forward_f64(a, h->m64.W, io->num_it, st);
+  }
+  if (e != hipSuccess) return hip_fail(e, "kernel launch");
+  return NRX_OK;
+}
+
+// Product-side restatement of the nearest-pilot positional encoding
+// (onnx_utils.py:206-260).  Pilots of CDM group g (DMRS config type 1)
+// occupy subcarriers f with f % 2 == g on the DMRS symbols.
+int nrx_compute_pe(int32_t num_tx, int32_t F, int32_t T, const int32_t* dmrs_symbols, int32_t nsym,
+                   const int32_t* cdm_group, float* pe) {
+  if (num_tx < 1 || F < 1 || T < 1 || !dmrs_symbols || nsym < 1 || !cdm_group || !pe)
+    return fail(NRX_ERR_INVALID_ARG, "bad argument");
+  std::vector<double> dt(T), df(F);
+  for (int u = 0; u < num_tx; ++u) {
+    if (cdm_group[u] != 0 && cdm_group[u] != 1) return fail(NRX_ERR_INVALID_ARG, "cdm_group must be 0/1");
+    bool any_f = false;
+    for (int t = 0; t < T; ++t) {
+      int best = 1 << 30;
+      for (int k = 0; k < nsym; ++k) best = std::min(best, std::abs(dmrs_symbols[k] - t));
+      dt[t] = best;
+    }
+    for (int f = 0; f < F; ++f) {
+      int best = 1 << 30;
+      for (int p = cdm_group[u]; p < F; p += 2) {
+        best = std::min(best, std::abs(p - f));
+        any_f = true;
+      }
+      df[f] = best;
+    }
+    if (!any_f) return fail(NRX_ERR_INVALID_ARG, "user has no pilots");
+    // normalise: time over the symbol axis, frequency over the subcarrier axis;
+    // population std, left unscaled where std == 0
+    auto norm = [](std::vector<double>& v) {
+      double m = 0;
+      for (double x : v) m += x;
+      m /= v.size();
+      double s2 = 0;
+      for (double& x : v) {
+        x -= m;
+        s2 += x * x;
+      }
+      const double sd = std::sqrt(s2 / v.size());
+      if (sd > 0)
+        for (double& x : v) x /= sd;
+    };
+    norm(dt);
+    norm(df);
+    for (int f = 0; f < F; ++f)
+      for (int t = 0; t < T; ++t) {
+        pe[(((size_t)u * F + f) * T + t) * 2 + 0] = (float)dt[t];
+        pe[(((size_t)u * F + f) * T + t) * 2 + 1] = (float)df[f];
+      }
+  }
+  return NRX_OK;
+}
+
+double nrx_flops_per_re_user(const nrx_desc* d, int32_t num_it) {
+  if (check_desc(d)) return 0.0;
+  auto sep = [](double ci, double co) { return 9 * ci + ci * co; };
+  const double init = sep(init_cin(d), kHID) + sep(kHID, kHID) + sep(kHID, kDS);
+  const double it = kDS * kAGG + kAGG * kDS + sep(2 * kDS + 2, kHID) + sep(kHID, kHID) + sep(kHID, kDS);
+  double heads = 0;
+  for (int h = 0; h < num_heads(d); ++h)
+    heads += kDS * kHID + kHID * (d->var_mcs_masking ? bits_max(d) : d->bits[h]);
+  const double ch = kDS * kHID + kHID * 2.0 * d->num_rx_ant;
+  return 2.0 * (init * num_init(d) + num_it * it + heads + ch);
+}
+
+}  // extern "C"

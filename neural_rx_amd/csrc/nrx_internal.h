@@ -1,0 +1,75 @@
+// nrx_internal.h -- shared between the HIP kernels and the host side of libnrx.so.
+//
+// Device data layout (see DESIGN.md "Data layout in HBM"):
+//   state / aggregate buffers  s, a : [B][U][F][16][64]   (t padded 14 -> 16 with zero
+//                                     rows, channels d_s = 56 padded to 64 with zeros)
+//   storage type: _Float16 (NRX_PREC_F16) or float (NRX_PREC_F32X)
+// Packed weights (one blob per precision, built by nrx_create):
+//   separable conv: dw [9][CINP] (tap = i*3 + j, i along F, j along T),
+//                   pwT [COUTP][CINP] (transposed pointwise kernel), bias [COUTP]
+//   dense:          wT [COUTP][CINP], bias [COUTP]
+//   WT = _Float16 / double, BT = float / double.  Zero padding everywhere.
+#pragma once
+#include <stdint.h>
+
+namespace nrx {
+
+constexpr int kT = 14;        // OFDM symbols (fixed by 5G NR slot)
+constexpr int kTP = 16;       // padded symbol axis = MFMA tile width
+constexpr int kDS = 56;       // state width d_s
+constexpr int kDSP = 64;      // padded state width
+constexpr int kHID = 128;     // conv hidden width / readout hidden width
+constexpr int kAGG = 64;      // aggregation hidden width
+constexpr int kUPD_CINP = 128;  // [a, s, pe] = 114 -> 128
+constexpr int kMaxInit = 8;
+constexpr int kMaxIt = 8;
+constexpr int kMaxHeads = 8;
+constexpr int kMaxUsers = 16;
+constexpr int kHalo = 3;      // 3 stacked 3x3 convs per block
+
+template <class WT, class BT>
+struct SepW {
+  const WT* dw;
+  const WT* pw;   // transposed [COUTP][CINP]
+  const BT* b;
+};
+
+template <class WT, class BT>
+struct DenseW {
+  const WT* w;    // transposed [COUTP][CINP]
+  const BT* b;
+};
+
+template <class WT, class BT>
+struct ModelW {
+  SepW<WT, BT> init[kMaxInit][3];
+  DenseW<WT, BT> agg[kMaxIt][2];
+  SepW<WT, BT> upd[kMaxIt][3];
+  DenseW<WT, BT> llr[kMaxHeads][2];
+  DenseW<WT, BT> chest[2];
+};
+
+// Shapes + pointers of one forward (kernel argument).
+template <class WT, class BT, class S>
+struct FwdArgs {
+  int B, U, F, A, M, H;            // H = number of LLR heads
+  int init_cinp;                   // padded StateInit input width
+  int num_init;
+  int masking;
+  int use_h;
+  int bits_max;
+  int head_bits[kMaxHeads];
+  const float* y;                  // [B][F][T][2A]
+  const float* pe;                 // [U][F][T][2]
+  const float* h_hat;              // [B][U][F][T][2A] or null
+  const float* active;             // [B][U]
+  const float* mcs_mask;           // [B][U][M] or null
+  float* llr;                      // [H][B][U][F][T][bits_max]
+  float* h_ref;                    // [B][U][F][T][2A] or null
+  double* norm;                    // [B] workspace
+  S* s_in;                         // [B][U][F][16][64]
+  S* s_out;
+  S* a;
+};
+
+}  // namespace nrx

@@ -1,0 +1,268 @@
+"""Python face of the engine, mirroring the reference's receiver interfaces.
+
+* ``CGNNEngine`` -- one ``libnrx.so`` handle; ``forward(y, pe, h_hat, active, mcs_mask)``
+  on device-resident torch tensors.
+* ``CGNN`` -- the reference's core layer call, ``CGNN.forward([y, pe, h_hat, active_tx,
+  mcs_ue_mask]) -> (llrs, h_hats)`` (neural_rx.py:544-595) with the ``num_it`` property
+  and its assertion (neural_rx.py:532-542).
+* ``NeuralReceiver`` -- the drop-in named by the north star:
+  ``NeuralReceiver.__call__(rx_grid, pe=None, active_dmrs=None, h_hat=None,
+  mcs_ue_mask=None, num_it=None, layout="sionna") -> llr`` reproducing both wrapper
+  layouts: Sionna/``CGNNOFDM.forward`` (neural_rx.py:813-881: ``y[:,0]``
+  permuted to ``[B,F,T,A]`` and split into real/imag channels) and Aerial/
+  ``NeuralReceiverONNX.forward`` (neural_rx.py:1773-1812: real/imag inputs, LLRs
+  permuted to ``[B,bits,U,F,T]`` and negated).
+
+PyTorch tensors are used only as device containers; all arithmetic of the forward pass
+runs in the HIP kernels of ``libnrx.so``.  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from .config import ModelSpec, NRXConfig, dmrs_symbols, get_config, spec_from_config, user_cdm_groups
+from . import weights as _weights
+
+NUM_SYMBOLS = 14
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def compute_pe(num_tx: int, num_subcarriers: int, dmrs_syms: Sequence[int],
+               cdm_groups: Sequence[int], num_symbols: int = NUM_SYMBOLS) -> np.ndarray:
+    """Nearest-pilot positional encoding ``[U, F, T, 2]`` via the C ABI
+    (``nrx_compute_pe``; reference formula onnx_utils.py:206-260)."""
+    lib = _lib.load()
+    pe = np.zeros((num_tx, num_subcarriers, num_symbols, 2), np.float32)
+    syms = (ctypes.c_int32 * len(dmrs_syms))(*dmrs_syms)
+    grp = (ctypes.c_int32 * num_tx)(*cdm_groups[:num_tx])
+    _lib.check(lib.nrx_compute_pe(num_tx, num_subcarriers, num_symbols, syms, len(dmrs_syms), grp,
+                                  pe.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+    return pe
+
+
+class CGNNEngine:
+    """Owns one engine handle (packed fp16 + fp64 weights on the device)."""
+
+    def __init__(self, spec: ModelSpec, weight_list: Sequence[np.ndarray], device: int = 0):
+        self.spec = spec
+        self.device = device
+        lib = _lib.load()
+        self._lib = lib
+        self._desc = _lib.make_desc(spec)
+        n = ctypes.c_int32()
+        _lib.check(lib.nrx_weight_layout(ctypes.byref(self._desc), ctypes.byref(n), None, 0))
+        sizes = (ctypes.c_int64 * n.value)()
+        _lib.check(lib.nrx_weight_layout(ctypes.byref(self._desc), ctypes.byref(n), sizes, n.value))
+        if len(weight_list) != n.value:
+            raise ValueError(f"expected {n.value} weight arrays, got {len(weight_list)}")
+        arrs = [np.ascontiguousarray(w, dtype=np.float32) for w in weight_list]
+        for i, (a, s) in enumerate(zip(arrs, sizes)):
+            if a.size != s:
+                raise ValueError(f"weight {i}: {a.shape} has {a.size} elements, expected {s}")
+        ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+        self._keep = arrs
+        h = ctypes.c_void_p()
+        _lib.check(lib.nrx_create(ctypes.byref(self._desc), ptrs, sizes, n.value, device,
+                                  ctypes.byref(h)))
+        self._h = h
+        self._ws = {}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.nrx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -------------------------------------------------------------- helpers
+    def flops_per_re_user(self, num_it: Optional[int] = None) -> float:
+        return float(self._lib.nrx_flops_per_re_user(ctypes.byref(self._desc),
+                                                     num_it or self.spec.num_it))
+
+    def workspace_bytes(self, batch, num_tx, num_subcarriers, precision="f16") -> int:
+        shape = _lib.nrx_shape(batch, num_tx, num_subcarriers, NUM_SYMBOLS)
+        out = ctypes.c_size_t()
+        _lib.check(self._lib.nrx_workspace_size(self._h, ctypes.byref(shape),
+                                                _lib.PRECISIONS[precision], ctypes.byref(out)))
+        return out.value
+
+    def _workspace(self, nbytes: int):
+        torch = _torch()
+        ws = self._ws.get("buf")
+        if ws is None or ws.numel() < nbytes:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{self.device}")
+            self._ws["buf"] = ws
+        return ws
+
+    def alloc_outputs(self, batch, num_tx, num_subcarriers, want_h=True):
+        torch = _torch()
+        sp = self.spec
+        dev = f"cuda:{self.device}"
+        llr = torch.empty((sp.num_llr_heads, batch, num_tx, num_subcarriers, NUM_SYMBOLS, sp.bits_max),
+                          dtype=torch.float32, device=dev)
+        h = (torch.empty((batch, num_tx, num_subcarriers, NUM_SYMBOLS, 2 * sp.num_rx_ant),
+                         dtype=torch.float32, device=dev) if want_h else None)
+        return llr, h
+
+    # -------------------------------------------------------------- forward
+    def forward(self, y, pe, h_hat, active, mcs_mask=None, num_it=None, precision="f16",
+                out=None, want_h=True, stream=None):
+        """All inputs are float32 CUDA tensors in the CGNN layout (see include/nrx.h).
+        Returns ``(llr [H,B,U,F,T,bits_max], h_ref [B,U,F,T,2A] or None)``."""
+        torch = _torch()
+        sp = self.spec
+        if y.dim() != 4 or y.shape[2] != NUM_SYMBOLS or y.shape[3] != 2 * sp.num_rx_ant:
+            raise ValueError(f"y must be [B,F,14,{2 * sp.num_rx_ant}], got {tuple(y.shape)}")
+        B, F = y.shape[0], y.shape[1]
+        U = active.shape[1]
+        if tuple(pe.shape) != (U, F, NUM_SYMBOLS, 2):
+            if pe.shape[0] >= U and tuple(pe.shape[1:]) == (F, NUM_SYMBOLS, 2):
+                pe = pe[:U]          # pe[:num_tx] (neural_rx.py:817)
+            else:
+                raise ValueError(f"pe must be [U,F,14,2], got {tuple(pe.shape)}")
+        if h_hat is not None and tuple(h_hat.shape) != (B, U, F, NUM_SYMBOLS, 2 * sp.num_rx_ant):
+            raise ValueError(f"h_hat has shape {tuple(h_hat.shape)}")
+        if mcs_mask is not None and tuple(mcs_mask.shape) != (B, U, sp.num_mcs):
+            mcs_mask = mcs_mask.expand(B, U, sp.num_mcs)
+        tensors = [y, pe, h_hat, active, mcs_mask]
+        for t in tensors:
+            if t is not None and (not t.is_cuda or t.dtype != torch.float32):
+                raise ValueError("inputs must be float32 CUDA tensors")
+        y, pe, h_hat, active, mcs_mask = [None if t is None else t.contiguous() for t in tensors]
+        if out is None:
+            out = self.alloc_outputs(B, U, F, want_h)
+        llr, h_ref = out
+        prec = _lib.PRECISIONS[precision]
+        nbytes = self.workspace_bytes(B, U, F, precision)
+        ws = self._workspace(nbytes)
+        io = _lib.nrx_io()
+        io.shape = _lib.nrx_shape(B, U, F, NUM_SYMBOLS)
+        io.num_it = sp.num_it if num_it is None else num_it
+        io.precision = prec
+        io.y, io.pe, io.active, io.llr = y.data_ptr(), pe.data_ptr(), active.data_ptr(), llr.data_ptr()
+        io.h_hat = h_hat.data_ptr() if h_hat is not None else None
+        io.mcs_mask = mcs_mask.data_ptr() if mcs_mask is not None else None
+        io.h_ref = h_ref.data_ptr() if h_ref is not None else None
+        if stream is None:
+            stream = torch.cuda.current_stream(y.device).cuda_stream
+        _lib.check(self._lib.nrx_forward(self._h, ctypes.byref(io), ws.data_ptr(), ws.numel(), stream))
+        # keep inputs alive until the stream consumed them
+        self._last_inputs = tensors
+        return llr, h_ref
+
+
+def spec_for(config: str | NRXConfig, num_rx_ant: Optional[int] = None) -> ModelSpec:
+    cfg = get_config(config) if isinstance(config, str) else config
+    return spec_from_config(cfg, num_rx_ant)
+
+
+class CGNN:
+    """Reference-shaped core layer (neural_rx.py:407-595) backed by the engine."""
+
+    def __init__(self, config: str | NRXConfig = "nrx_rt", weight_list=None, device: int = 0,
+                 precision: str = "f16", num_rx_ant: Optional[int] = None):
+        self.cfg = get_config(config) if isinstance(config, str) else config
+        self.spec = spec_from_config(self.cfg, num_rx_ant)
+        if weight_list is None:
+            weight_list = _weights.load(self.cfg.label)
+        self.engine = CGNNEngine(self.spec, weight_list, device)
+        self.precision = precision
+        self._num_it = self.cfg.num_nrx_iter_eval
+
+    @property
+    def num_it(self):
+        return self._num_it
+
+    @num_it.setter
+    def num_it(self, val):
+        assert (val >= 1) and (val <= self.spec.num_it), "Invalid number of iterations"
+        self._num_it = val
+
+    def forward(self, inputs):
+        """``inputs = [y, pe, h_hat, active_tx, mcs_ue_mask]`` -> ``(llrs, h_hats)`` with
+        ``llrs[-1][m]`` = LLRs of MCS m ``[B,U,F,T,bits_m]`` and ``h_hats[-1]``."""
+        y, pe, h_hat, active_tx, mcs_ue_mask = inputs
+        llr, h = self.engine.forward(y, pe, h_hat, active_tx, mcs_ue_mask, self._num_it,
+                                     self.precision)
+        sp = self.spec
+        per_mcs = []
+        for m, nb in enumerate(sp.bits):
+            head = 0 if sp.masking else m
+            per_mcs.append(llr[head, ..., :nb])
+        return [per_mcs], [h]
+
+    __call__ = forward
+
+
+class NeuralReceiver:
+    """Drop-in receiver: rx grid + PE + active DMRS ports (+ h_hat) -> LLRs."""
+
+    def __init__(self, config: str | NRXConfig = "nrx_rt", weight_list=None, device: int = 0,
+                 precision: str = "f16", num_rx_ant: Optional[int] = None,
+                 cdm_groups: Optional[Sequence[int]] = None):
+        self.cgnn = CGNN(config, weight_list, device, precision, num_rx_ant)
+        self.cfg = self.cgnn.cfg
+        self.spec = self.cgnn.spec
+        self.device = device
+        self._cdm_groups = cdm_groups
+        self._pe_cache = {}
+
+    @property
+    def num_it(self):
+        return self.cgnn.num_it
+
+    @num_it.setter
+    def num_it(self, val):
+        self.cgnn.num_it = val
+
+    def positional_encoding(self, num_tx: int, num_subcarriers: int):
+        torch = _torch()
+        key = (num_tx, num_subcarriers)
+        if key not in self._pe_cache:
+            groups = self._cdm_groups or user_cdm_groups(self.cfg, num_tx)
+            pe = compute_pe(num_tx, num_subcarriers, dmrs_symbols(self.cfg), groups)
+            self._pe_cache[key] = torch.from_numpy(pe).to(f"cuda:{self.device}")
+        return self._pe_cache[key]
+
+    def __call__(self, rx_grid, pe=None, active_dmrs=None, h_hat=None, mcs_ue_mask=None,
+                 num_it=None, layout: str = "sionna", return_h_hat: bool = False):
+        torch = _torch()
+        if num_it is not None:
+            self.num_it = num_it
+        if layout == "sionna":
+            # CGNNOFDM.forward: y [B,1,A,T,F] complex -> [B,F,T,2A] (neural_rx.py:831-833)
+            y = rx_grid[:, 0].permute(0, 3, 2, 1)
+            y = torch.cat([y.real, y.imag], dim=-1).to(torch.float32).contiguous()
+        elif layout == "aerial":
+            # NeuralReceiverONNX.forward: (rx_slot_real, rx_slot_imag) [B,F,T,A]
+            y_re, y_im = rx_grid
+            y = torch.cat([y_re, y_im], dim=-1).to(torch.float32).contiguous()
+        elif layout == "cgnn":
+            y = rx_grid
+        else:
+            raise ValueError(f"unknown layout {layout}")
+        B, F = y.shape[0], y.shape[1]
+        if active_dmrs is None:
+            active_dmrs = torch.ones((B, self.cfg.max_num_tx), dtype=torch.float32, device=y.device)
+        active = active_dmrs.to(torch.float32).contiguous()
+        U = active.shape[1]
+        if pe is None:
+            pe = self.positional_encoding(U, F)
+        llrs, h_hats = self.cgnn([y, pe, h_hat, active, mcs_ue_mask])
+        llr = llrs[-1][0] if self.spec.num_mcs == 1 else llrs[-1]
+        h_ref = h_hats[-1]
+        if layout == "aerial":
+            llr = -llr.permute(0, 4, 1, 2, 3)   # [B,bits,U,F,T], LLR = log p0/p1
+        return (llr, h_ref) if return_h_hat else llr

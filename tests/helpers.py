@@ -1,0 +1,92 @@
+"""Shared test fixtures: seeded cases run through the oracle and the engine."""
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional, Sequence
+
+import numpy as np
+
+from neural_rx_amd import synth
+from neural_rx_amd import weights as W
+from neural_rx_amd.config import dmrs_symbols, get_config, spec_from_config, user_cdm_groups
+from oracle import cgnn_ref, pe_ref
+
+
+@dataclasses.dataclass
+class Case:
+    name: str
+    cfg: object
+    spec: object
+    weights: list
+    y: np.ndarray
+    pe: np.ndarray
+    h_hat: Optional[np.ndarray]
+    active: np.ndarray
+    mcs_mask: Optional[np.ndarray]
+    slots: Optional[synth.Slots] = None
+    num_it: Optional[int] = None
+
+
+def make_case(config="nrx_rt", batch=2, users=2, prbs=4, snr_db=15.0, seed=1,
+              active=None, mcs_choice: Optional[Sequence[int]] = None, num_rx_ant=None,
+              random_inputs=False, num_it=None, seeded_weights=False) -> Case:
+    cfg = get_config(config)
+    spec = spec_from_config(cfg, num_rx_ant)
+    weights = W.seeded(spec, seed=seed) if seeded_weights else W.load(cfg.label)
+    groups = user_cdm_groups(cfg, users)
+    f = 12 * prbs
+    pe = pe_ref.pe_for_groups(f, 14, dmrs_symbols(cfg), groups)
+    rng = np.random.default_rng(seed + 100)
+    if mcs_choice is None:
+        mcs_choice = rng.integers(0, spec.num_mcs, size=(batch, users))
+    mcs_choice = np.asarray(mcs_choice).reshape(batch, users)
+    mask = np.eye(spec.num_mcs, dtype=np.float32)[mcs_choice]
+    if active is None:
+        active = np.ones((batch, users), np.float32)
+    active = np.asarray(active, np.float32)
+    slots = None
+    if random_inputs:
+        a2 = 2 * spec.num_rx_ant
+        y = rng.standard_normal((batch, f, 14, a2)).astype(np.float32)
+        h = rng.standard_normal((batch, users, f, 14, a2)).astype(np.float32)
+    else:
+        bits = [spec.bits[mcs_choice[0, u]] for u in range(users)]
+        slots = synth.generate(batch, users, prbs, spec.num_rx_ant, bits, groups,
+                               dmrs_symbols(cfg), snr_db=snr_db, seed=seed, active=active)
+        y, h = slots.y, slots.h_hat
+    return Case(config, cfg, spec, weights, y, pe, h, active, mask, slots, num_it)
+
+
+def run_oracle(case: Case, dtype=np.float64):
+    w = cgnn_ref.split_keras_weights(case.weights, case.spec)
+    return cgnn_ref.cgnn_forward(case.y, case.pe, case.h_hat, case.active, case.mcs_mask, w,
+                                 case.spec, num_it=case.num_it, dtype=dtype)
+
+
+def run_engine(case: Case, precision="f16", engine=None):
+    import torch
+    from neural_rx_amd.receiver import CGNNEngine
+    eng = engine or CGNNEngine(case.spec, case.weights)
+    dev = "cuda:0"
+    t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)
+    llr, h = eng.forward(t(case.y), t(case.pe), t(case.h_hat), t(case.active), t(case.mcs_mask),
+                         num_it=case.num_it, precision=precision)
+    torch.cuda.synchronize()
+    llr = llr.cpu().numpy()
+    sp = case.spec
+    per_mcs = [llr[0 if sp.masking else m, ..., :nb] for m, nb in enumerate(sp.bits)]
+    return {"llr": per_mcs, "llr_raw": llr, "h_hat": h.cpu().numpy()}
+
+
+def compare(ref, got):
+    """max-abs LLR / h errors, relative-to-max error and hard-decision disagreement."""
+    out = {}
+    lmax = max(float(np.abs(r).max()) for r in ref["llr"])
+    errs = [float(np.abs(r - g).max()) for r, g in zip(ref["llr"], got["llr"])]
+    flips = [float((np.sign(r) != np.sign(g)).mean()) for r, g in zip(ref["llr"], got["llr"])]
+    out["llr_maxabs"] = max(errs)
+    out["llr_rel"] = max(errs) / max(lmax, 1e-12)
+    out["flip_rate"] = max(flips)
+    out["h_maxabs"] = float(np.abs(ref["h_hat"] - got["h_hat"]).max())
+    out["llr_max"] = lmax
+    return out
