@@ -1,0 +1,277 @@
+#!/usr/bin/env python3
+"""Benchmark of the CGNN neural-receiver forward pass on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1]): nrx_rt weights, 2 users, 4 PRB (F = 48), 4 rx
+antennas, 16-QAM, batch 128 slots per GPU, f16 perf mode.  A "step" = one full CGNN
+forward (norm, StateInit, 2 x [aggregation, state update], readouts) over the batch,
+inputs already resident in HBM.  Multi-GPU: each rank runs its own 128-slot shard
+(independent slots, no collective on the data path -> weak scaling); one RCCL
+all-reduce of the per-rank elapsed time (MAX) after the timed region.
+
+Prints ONE JSON line (rank 0) with the headline metric (slots/s, whole job), the
+per-slot p50 latency at batch 1, the roofline of the dominant kernel
+(state update, measured with HIP events on the launch stream) and a CPU baseline
+(the numpy oracle, fp32, timed on a bounded sample on this host).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--config", default="nrx_rt")
+    p.add_argument("--batch", type=int, default=128, help="slots per GPU per step")
+    p.add_argument("--users", type=int, default=2)
+    p.add_argument("--prbs", type=int, default=4)
+    p.add_argument("--precision", default="f16", choices=["f16", "f32x"])
+    p.add_argument("--latency-iters", type=int, default=1000)
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-latency", action="store_true")
+    p.add_argument("--profile-only", action="store_true",
+                   help="run warmup + timed steps only (for rocprofv3)")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    device = local_rank if world > 1 else 0
+    torch.cuda.set_device(device)
+    dev = f"cuda:{device}"
+
+    from neural_rx_amd import metrics, synth
+    from neural_rx_amd import weights as W
+    from neural_rx_amd.config import dmrs_symbols, get_config, spec_from_config, user_cdm_groups
+    from neural_rx_amd.receiver import CGNNEngine, compute_pe
+
+    cfg = get_config(args.config)
+    spec = spec_from_config(cfg)
+    groups = user_cdm_groups(cfg, args.users)
+    F = 12 * args.prbs
+    B, U = args.batch, args.users
+    num_it = cfg.num_nrx_iter_eval
+    bits = [spec.bits[0]] * U
+    slots = synth.generate(B, U, args.prbs, spec.num_rx_ant, bits, groups, dmrs_symbols(cfg),
+                           snr_db=10.0, seed=1234 + 2 + 1000 * rank)
+    pe_np = compute_pe(U, F, dmrs_symbols(cfg), groups)
+    eng = CGNNEngine(spec, W.load(cfg.label), device)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)
+    y, h, act, pe = t(slots.y), t(slots.h_hat), t(slots.active), t(pe_np)
+    out = eng.alloc_outputs(B, U, F)
+
+    def step():
+        eng.forward(y, pe, h, act, None, num_it, args.precision, out=out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    if args.profile_only:
+        if rank == 0:
+            print(json.dumps({"profile_only": True, "ms_per_step": 1e3 * elapsed / args.steps}))
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    slots_total = world * B * args.steps
+    value = slots_total / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # ---- roofline of the dominant kernel: HIP events around each launch, on the
+    # launch stream, over a second timed region of the same length
+    kflops = metrics.kernel_flops_per_re_user(spec)
+    re_users = B * U * F * 14
+    eng.profile(True)
+    for _ in range(args.steps):
+        step()
+    prof = eng.profile_read()
+    eng.profile(False)
+    kern = {}
+    for name, (n, ms) in prof.items():
+        if n:
+            avg_s = ms / n * 1e-3
+            fl = kflops[name] * re_users
+            kern[name] = {"launches": n, "avg_us": round(avg_s * 1e6, 3),
+                          "tflops": round(fl / avg_s / 1e12, 2) if fl else None}
+    dom = "state_update"
+    dom_avg_s = prof[dom][1] / prof[dom][0] * 1e-3
+    dom_flops = kflops[dom] * re_users
+    peak = metrics.PEAK_TFLOPS[args.precision]
+    achieved = dom_flops / dom_avg_s / 1e12
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            key = f"{args.config}_b{B}_u{U}_p{args.prbs}_{args.precision}"
+            traffic = pmc.get(key, {}).get("k_update_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": traffic,
+                "kernel": "k_update", "flops_per_launch": dom_flops,
+                "avg_launch_us": round(dom_avg_s * 1e6, 3)}
+    whole_tflops = metrics.forward_flops_per_re_user(spec, num_it) * re_users * world / (elapsed / args.steps) / 1e12
+
+    # ---- batch-1 per-slot latency (hipGraph replay; device-only and H2D+compute+D2H)
+    latency = None
+    if not args.no_latency and rank == 0:
+        latency = measure_latency(torch, eng, spec, cfg, args, groups, dev, num_it)
+
+    # ---- CPU baseline: the numpy oracle (fp32) on a bounded sample of the same workload
+    cpu = None
+    if not args.no_cpu_baseline and rank == 0 and world == 1:
+        cpu = cpu_baseline(spec, cfg, slots, pe_np, args, num_it)
+
+    if rank == 0:
+        line = {
+            "metric": "5G NR slots/sec + p50 per-slot latency, nrx_rt config",
+            "value": round(value, 1),
+            "unit": "slots/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f16" if args.precision == "f16" else "f32/f64",
+            "data": "synthetic (seeded PUSCH slots: 16-QAM, DMRS type 1, TDL channel, LS+NN h_hat; trained nrx_rt weights)",
+            "config": {"workload": f"{args.config}, {U} users, {args.prbs} PRB, 4 rx_ant, 16-QAM, "
+                                   f"batch={B} slots per GPU",
+                       "global_batch": B * world, "num_it": num_it, "parallelism": f"dp{world} (slot shards)"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "p50_latency_ms": latency,
+            "whole_forward_tflops": round(whole_tflops, 2),
+            "kernels": kern,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def measure_latency(torch, eng, spec, cfg, args, groups, dev, num_it):
+    from neural_rx_amd import synth
+    from neural_rx_amd.config import dmrs_symbols
+    from neural_rx_amd.receiver import compute_pe
+    res = {}
+    for tag, prbs in (("4prb", args.prbs), ("132prb_trt_shape", 132)):
+        F = 12 * prbs
+        U = args.users
+        s = synth.generate(1, U, prbs, spec.num_rx_ant, [spec.bits[0]] * U, groups,
+                           dmrs_symbols(cfg), snr_db=10.0, seed=77)
+        pe = torch.from_numpy(compute_pe(U, F, dmrs_symbols(cfg), groups)).to(dev)
+        hy = torch.from_numpy(s.y).pin_memory()
+        hh = torch.from_numpy(s.h_hat).pin_memory()
+        ha = torch.from_numpy(s.active).pin_memory()
+        y = hy.to(dev)
+        h = hh.to(dev)
+        a = ha.to(dev)
+        out = eng.alloc_outputs(1, U, F)
+        host_llr = torch.empty(out[0].shape, dtype=torch.float32).pin_memory()
+        stream = torch.cuda.Stream(device=dev)
+        with torch.cuda.stream(stream):
+            for _ in range(3):
+                eng.forward(y, pe, h, a, None, num_it, args.precision, out=out)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            eng.forward(y, pe, h, a, None, num_it, args.precision, out=out)
+        torch.cuda.synchronize()
+        n = args.latency_iters
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+        with torch.cuda.stream(stream):
+            for i in range(n):
+                ev[i][0].record(stream)
+                g.replay()
+                ev[i][1].record(stream)
+        torch.cuda.synchronize()
+        dev_ms = np.array([a_.elapsed_time(b_) for a_, b_ in ev])
+        e2e = []
+        with torch.cuda.stream(stream):
+            for i in range(n):
+                t0 = time.perf_counter()
+                y.copy_(hy, non_blocking=True)
+                h.copy_(hh, non_blocking=True)
+                a.copy_(ha, non_blocking=True)
+                g.replay()
+                host_llr.copy_(out[0], non_blocking=True)
+                stream.synchronize()
+                e2e.append(time.perf_counter() - t0)
+        e2e = np.array(e2e) * 1e3
+        res[tag] = {"device_p50": round(float(np.median(dev_ms)), 4),
+                    "e2e_p50": round(float(np.median(e2e)), 4),
+                    "e2e_p99": round(float(np.percentile(e2e, 99)), 4),
+                    "batch1_slots_per_s_e2e": round(1e3 / float(np.median(e2e)), 1)}
+    return res
+
+
+def cpu_baseline(spec, cfg, slots, pe_np, args, num_it):
+    from oracle import cgnn_ref
+    from neural_rx_amd import weights as W
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        threads = 1
+    w = cgnn_ref.split_keras_weights(W.load(cfg.label), spec)
+    nb = min(4, slots.y.shape[0])
+    y, h, a = slots.y[:nb], slots.h_hat[:nb], slots.active[:nb]
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        cgnn_ref.cgnn_forward(y, pe_np, h, a, np.ones((nb, a.shape[1], 1), np.float32), w, spec,
+                              num_it=num_it, dtype=np.float32)
+        done += nb
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds:
+            break
+    import platform
+    return {"value": round(done / el, 2), "unit": "slots/s", "cores": threads, "kind": "port",
+            "sample": f"numpy fp32 oracle (oracle/cgnn_ref.py), {done} slots of the bench workload "
+                      f"({nb}-slot batches, {args.users} users, {args.prbs} PRB) in {el:.1f} s; "
+                      f"BLAS threads={threads}; cpu={platform.processor() or platform.machine()}"}
+
+
+if __name__ == "__main__":
+    main()

@@ -22,7 +22,9 @@ PRECISIONS = {"f16": NRX_PREC_F16, "fp16": NRX_PREC_F16, "f32x": NRX_PREC_F32X,
 EXPORTS = [
     "nrx_create", "nrx_weight_layout", "nrx_workspace_size", "nrx_forward", "nrx_destroy",
     "nrx_compute_pe", "nrx_flops_per_re_user", "nrx_last_error", "nrx_api_version",
+    "nrx_profile_enable", "nrx_profile_read",
 ]
+KERNELS = ["norm", "state_init", "aggregate", "state_update", "readout"]
 
 
 class NRXLibraryError(RuntimeError):
@@ -87,6 +89,13 @@ def load(path: str = LIB_PATH):
         raise NRXLibraryError(
             f"{path} not found: the MI355X engine is not built "
             "(run `python -m neural_rx_amd.build`); there is no CPU fallback")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7.  Load
+    # torch first so that libnrx's DT_NEEDED libamdhip64.so.7 binds to that copy
+    # (by soname) instead of pulling /opt/rocm's as a second runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover - plain C users
+        pass
     try:
         lib = ctypes.CDLL(path)
     except OSError as e:  # pragma: no cover - depends on the box
@@ -111,6 +120,10 @@ def load(path: str = LIB_PATH):
     lib.nrx_flops_per_re_user.restype = c.c_double
     lib.nrx_last_error.argtypes = []
     lib.nrx_last_error.restype = c.c_char_p
+    lib.nrx_profile_enable.argtypes = [c.c_void_p, c.c_int32]
+    lib.nrx_profile_enable.restype = c.c_int
+    lib.nrx_profile_read.argtypes = [c.c_void_p, c.c_int32, P(c.c_int64), P(c.c_double)]
+    lib.nrx_profile_read.restype = c.c_int
     lib.nrx_api_version.argtypes = []
     lib.nrx_api_version.restype = c.c_int32
     _lib = lib

@@ -19,9 +19,11 @@
 
 namespace nrx {
 hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args,
-                              const ModelW<_Float16, float>& W, int num_it, hipStream_t st);
+                              const ModelW<_Float16, float>& W, int num_it, hipStream_t st,
+                              Prof* prof);
 hipError_t launch_forward_f64(const FwdArgs<double, double, float>& args,
-                              const ModelW<double, double>& W, int num_it, hipStream_t st);
+                              const ModelW<double, double>& W, int num_it, hipStream_t st,
+                              Prof* prof);
 hipError_t setup_kernels();
 int strip_width(int precision);
 }  // namespace nrx
@@ -242,11 +244,70 @@ int build_model(const nrx_desc* d, const float* const* w, int kc, DeviceModel<WT
 
 }  // namespace
 
+// Event-pair recorder behind nrx_profile_enable / nrx_profile_read.
+struct EventProf : Prof {
+  struct Rec { int kid; hipEvent_t a, b; };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  hipEvent_t get() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  void begin(int kid, void* st) override {
+    Rec r{kid, get(), nullptr};
+    (void)hipEventRecord(r.a, (hipStream_t)st);
+    recs.push_back(r);
+  }
+  void end(int, void* st) override {
+    hipEvent_t e = get();
+    (void)hipEventRecord(e, (hipStream_t)st);
+    recs.back().b = e;
+  }
+  // fold finished records into totals
+  int64_t launches[K_COUNT] = {0};
+  double total_ms[K_COUNT] = {0};
+  hipError_t collect() {
+    for (auto& r : recs) {
+      hipError_t e = hipEventSynchronize(r.b);
+      if (e != hipSuccess) return e;
+      float ms = 0.f;
+      e = hipEventElapsedTime(&ms, r.a, r.b);
+      if (e != hipSuccess) return e;
+      launches[r.kid] += 1;
+      total_ms[r.kid] += ms;
+      pool.push_back(r.a);
+      pool.push_back(r.b);
+    }
+    recs.clear();
+    return hipSuccess;
+  }
+  void reset() {
+    for (int k = 0; k < K_COUNT; ++k) {
+      launches[k] = 0;
+      total_ms[k] = 0;
+    }
+  }
+  ~EventProf() override {
+    for (auto& r : recs) {
+      (void)hipEventDestroy(r.a);
+      if (r.b) (void)hipEventDestroy(r.b);
+    }
+    for (auto e : pool) (void)hipEventDestroy(e);
+  }
+};
+
 struct nrx_handle {
   nrx_desc desc;
   int device;
   DeviceModel<_Float16, float> m16;
   DeviceModel<double, double> m64;
+  EventProf* prof = nullptr;
 };
 
 static size_t state_bytes(const nrx_shape* s, int precision) {
@@ -350,6 +411,7 @@ void nrx_destroy(nrx_handle* h) {
   if (!h) return;
   if (h->m16.dev) (void)hipFree(h->m16.dev);
   if (h->m64.dev) (void)hipFree(h->m64.dev);
+  delete h->prof;
   delete h;
 }
 
@@ -381,13 +443,38 @@ int nrx_forward(nrx_handle* h, const nrx_io* io, void* workspace, size_t workspa
   if (io->precision == NRX_PREC_F16) {
     FwdArgs<_Float16, float, _Float16> a{};
     fill_args(a, h, io, workspace, h->m16.init_cinp);
-    e = launch_forward_f16(a, h->m16.W, io->num_it, st);
+    e = launch_forward_f16(a, h->m16.W, io->num_it, st, h->prof);
   } else {
     FwdArgs<double, double, float> a{};
     fill_args(a, h, io, workspace, h->m64.init_cinp);
-    e = launch_forward_f64(a, h->m64.W, io->num_it, st);
+    e = launch_forward_f64(a, h->m64.W, io->num_it, st, h->prof);
   }
   if (e != hipSuccess) return hip_fail(e, "kernel launch");
+  return NRX_OK;
+}
+
+int nrx_profile_enable(nrx_handle* h, int32_t enable) {
+  if (!h) return fail(NRX_ERR_INVALID_ARG, "null handle");
+  if (enable) {
+    if (!h->prof) h->prof = new EventProf();
+    hipError_t e = h->prof->collect();
+    h->prof->reset();
+    if (e != hipSuccess) return hip_fail(e, "profile reset");
+  } else {
+    delete h->prof;
+    h->prof = nullptr;
+  }
+  return NRX_OK;
+}
+
+int nrx_profile_read(nrx_handle* h, int32_t kernel, int64_t* launches, double* total_ms) {
+  if (!h || !launches || !total_ms) return fail(NRX_ERR_INVALID_ARG, "null argument");
+  if (kernel < 0 || kernel >= K_COUNT) return fail(NRX_ERR_INVALID_ARG, "bad kernel id");
+  if (!h->prof) return fail(NRX_ERR_INVALID_ARG, "profiling is not enabled");
+  hipError_t e = h->prof->collect();
+  if (e != hipSuccess) return hip_fail(e, "profile collect");
+  *launches = h->prof->launches[kernel];
+  *total_ms = h->prof->total_ms[kernel];
   return NRX_OK;
 }
 

@@ -72,4 +72,14 @@ struct FwdArgs {
   S* a;
 };
 
+// Optional per-kernel timing (nrx_profile_enable): events recorded around each launch on
+// the launch stream.  Kernel ids:
+enum KernelId { K_NORM = 0, K_INIT = 1, K_AGG = 2, K_UPDATE = 3, K_READOUT = 4, K_COUNT = 5 };
+
+struct Prof {
+  virtual void begin(int kid, void* stream) = 0;
+  virtual void end(int kid, void* stream) = 0;
+  virtual ~Prof() {}
+};
+
 }  // namespace nrx

@@ -616,10 +616,15 @@ struct Launch {
     return e;
   }
 
-  static hipError_t run(const A& args0, const MW& W, int num_it, hipStream_t st) {
+  static hipError_t run(const A& args0, const MW& W, int num_it, hipStream_t st, Prof* prof) {
     A args = args0;
     const int strips = (args.F + P::FO - 1) / P::FO;
+    auto B_ = [&](int k) { if (prof) prof->begin(k, st); };
+    auto E_ = [&](int k) { if (prof) prof->end(k, st); };
+    B_(K_NORM);
     k_norm<<<args.B, 256, 0, st>>>(args.y, args.F * kT * 2 * args.A, args.norm);
+    E_(K_NORM);
+    B_(K_INIT);
     {
       InitParams<P> ip;
       ip.a = args;
@@ -637,6 +642,7 @@ struct Launch {
         k_init<P, 128><<<grid, 512, L, st>>>(ip);
       }
     }
+    E_(K_INIT);
     constexpr int LU = strip_lds_bytes<P>(kUPD_CINP);
     for (int i = 0; i < num_it; ++i) {
       // s_out of the previous stage is this iteration's input
@@ -645,11 +651,15 @@ struct Launch {
       ap.a = args;
       ap.w[0] = W.agg[i][0];
       ap.w[1] = W.agg[i][1];
+      B_(K_AGG);
       k_agg<P><<<dim3((args.F + 3) / 4, args.B), 256, 0, st>>>(ap);
+      E_(K_AGG);
       UpdParams<P> up;
       up.a = args;
       for (int l = 0; l < 3; ++l) up.w[l] = W.upd[i][l];
+      B_(K_UPDATE);
       k_update<P><<<dim3(strips, args.U, args.B), 512, LU, st>>>(up);
+      E_(K_UPDATE);
     }
     std::swap(args.s_in, args.s_out);
     ReadParams<P> rp;
@@ -661,20 +671,24 @@ struct Launch {
     rp.chest[0] = W.chest[0];
     rp.chest[1] = W.chest[1];
     dim3 grid((args.F + 3) / 4, args.U, args.B);
+    B_(K_READOUT);
     if (2 * args.A <= 16) k_readout<P, 16><<<grid, 256, 0, st>>>(rp);
     else k_readout<P, 32><<<grid, 256, 0, st>>>(rp);
+    E_(K_READOUT);
     return hipGetLastError();
   }
 };
 
 hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args,
-                              const ModelW<_Float16, float>& W, int num_it, hipStream_t st) {
-  return Launch<P16>::run(args, W, num_it, st);
+                              const ModelW<_Float16, float>& W, int num_it, hipStream_t st,
+                              Prof* prof) {
+  return Launch<P16>::run(args, W, num_it, st, prof);
 }
 
 hipError_t launch_forward_f64(const FwdArgs<double, double, float>& args,
-                              const ModelW<double, double>& W, int num_it, hipStream_t st) {
-  return Launch<P64>::run(args, W, num_it, st);
+                              const ModelW<double, double>& W, int num_it, hipStream_t st,
+                              Prof* prof) {
+  return Launch<P64>::run(args, W, num_it, st, prof);
 }
 
 hipError_t setup_kernels() {

@@ -1,0 +1,46 @@
+"""Algorithmic work per kernel.
+
+FLOPs count 2 per multiply-accumulate of the reference network, per resource element
+(RE = one subcarrier x one OFDM symbol, T = 14, no padding) and per user; padding
+work (T 14 -> 16, channels 56 -> 64 / 114 -> 128 / bits -> 16) is real work the
+kernels do but is NOT counted, so it shows up as lost roofline fraction.
+``sep(ci, co) = 9 ci + ci co`` (depthwise 3x3 + pointwise).
+"""
+from __future__ import annotations
+
+from .config import ModelSpec
+
+
+def sep(ci: int, co: int) -> int:
+    return 9 * ci + ci * co
+
+
+def kernel_flops_per_re_user(spec: ModelSpec) -> dict:
+    u1, u2 = spec.init_units
+    v1, v2 = spec.state_units
+    init = 2 * spec.num_init * (sep(spec.init_in_ch, u1) + sep(u1, u2) + sep(u2, spec.d_s))
+    agg = 2 * (spec.d_s * spec.agg_units + spec.agg_units * spec.d_s)
+    upd = 2 * (sep(spec.update_in_ch, v1) + sep(v1, v2) + sep(v2, spec.d_s))
+    ro = 2 * (sum(spec.d_s * spec.readout_units + spec.readout_units * b for b in spec.head_bits)
+              + spec.d_s * spec.readout_units + spec.readout_units * 2 * spec.num_rx_ant)
+    return {"norm": 0, "state_init": init, "aggregate": agg, "state_update": upd, "readout": ro}
+
+
+def forward_flops_per_re_user(spec: ModelSpec, num_it: int) -> int:
+    k = kernel_flops_per_re_user(spec)
+    return k["state_init"] + num_it * (k["aggregate"] + k["state_update"]) + k["readout"]
+
+
+def io_bytes_per_slot(spec: ModelSpec, num_tx: int, num_subcarriers: int, elem: int = 4,
+                      with_h: bool = True) -> dict:
+    """Compulsory HBM bytes of one slot: inputs y, h_hat, pe and outputs llr (+ h_ref)."""
+    re = num_subcarriers * 14
+    a2 = 2 * spec.num_rx_ant
+    inp = re * a2 * elem + num_tx * re * a2 * elem + num_tx * re * 2 * elem
+    out = num_tx * re * spec.bits_max * 4 * spec.num_llr_heads + (num_tx * re * a2 * 4 if with_h else 0)
+    return {"in": inp, "out": out}
+
+
+# MI355X peaks (MI355X_MICROARCH.md "Chip-level parameters")
+PEAK_TFLOPS = {"f16": 2500.0, "f32x": 78.6}   # dense f16 MFMA; f64 MFMA (spec, = FP32/2)
+PEAK_HBM_GBS = 8000.0

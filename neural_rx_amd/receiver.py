@@ -86,6 +86,19 @@ class CGNNEngine:
         except Exception:
             pass
 
+    # -------------------------------------------------------------- profiling
+    def profile(self, enable: bool = True):
+        _lib.check(self._lib.nrx_profile_enable(self._h, int(enable)))
+
+    def profile_read(self):
+        """{kernel: (launches, total_ms)} since the last profile(True)."""
+        out = {}
+        for k, name in enumerate(_lib.KERNELS):
+            n, ms = ctypes.c_int64(), ctypes.c_double()
+            _lib.check(self._lib.nrx_profile_read(self._h, k, ctypes.byref(n), ctypes.byref(ms)))
+            out[name] = (n.value, ms.value)
+        return out
+
     # -------------------------------------------------------------- helpers
     def flops_per_re_user(self, num_it: Optional[int] = None) -> float:
         return float(self._lib.nrx_flops_per_re_user(ctypes.byref(self._desc),

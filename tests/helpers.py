@@ -89,4 +89,11 @@ def compare(ref, got):
     out["flip_rate"] = max(flips)
     out["h_maxabs"] = float(np.abs(ref["h_hat"] - got["h_hat"]).max())
     out["llr_max"] = lmax
+    # hard-decision disagreement restricted to confident reference bits
+    conf = [float((np.sign(r) != np.sign(g))[np.abs(r) > 0.5].mean()) if (np.abs(r) > 0.5).any() else 0.0
+            for r, g in zip(ref["llr"], got["llr"])]
+    out["flip_rate_confident"] = max(conf)
+    rms = [float(np.sqrt(np.mean((r - g) ** 2)) / max(np.sqrt(np.mean(r ** 2)), 1e-12))
+           for r, g in zip(ref["llr"], got["llr"])]
+    out["llr_rms_rel"] = max(rms)
     return out
