@@ -118,7 +118,7 @@ def main():
 
     # ---- roofline of the dominant kernel: HIP events around each launch, on the
     # launch stream, over a second timed region of the same length
-    kflops = metrics.kernel_flops_per_re_user(spec)
+    kflops = metrics.launch_flops_per_re_user(spec, num_it)
     re_users = B * U * F * 14
     eng.profile(True)
     for _ in range(args.steps):
@@ -148,7 +148,8 @@ def main():
             traffic = None
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
-                "kernel": "k_update", "flops_per_launch": dom_flops,
+                "kernel": "k_update (3 sep-convs + fused aggregation/readout tail)",
+                "flops_per_launch": dom_flops,
                 "avg_launch_us": round(dom_avg_s * 1e6, 3)}
     whole_tflops = metrics.forward_flops_per_re_user(spec, num_it) * re_users * world / (elapsed / args.steps) / 1e12
 

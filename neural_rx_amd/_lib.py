@@ -24,7 +24,7 @@ EXPORTS = [
     "nrx_compute_pe", "nrx_flops_per_re_user", "nrx_last_error", "nrx_api_version",
     "nrx_profile_enable", "nrx_profile_read",
 ]
-KERNELS = ["norm", "state_init", "aggregate", "state_update", "readout"]
+KERNELS = ["norm", "state_init", "state_update"]
 
 
 class NRXLibraryError(RuntimeError):

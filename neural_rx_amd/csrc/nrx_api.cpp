@@ -61,6 +61,8 @@ int check_desc(const nrx_desc* d) {
   if (d->num_mcs < 1 || d->num_mcs > kMaxHeads) return fail(NRX_ERR_UNSUPPORTED, "num_mcs must be 1..8");
   for (int m = 0; m < d->num_mcs; ++m)
     if (d->bits[m] < 1 || d->bits[m] > 8) return fail(NRX_ERR_UNSUPPORTED, "bits must be 1..8");
+  if (!d->var_mcs_masking && d->num_mcs > 3)
+    return fail(NRX_ERR_UNSUPPORTED, "at most 3 LLR heads (fused readout staging)");
   if (d->use_h_hat != 0 && d->use_h_hat != 1) return fail(NRX_ERR_INVALID_ARG, "use_h_hat must be 0/1");
   return NRX_OK;
 }
@@ -155,11 +157,22 @@ struct Packer {
     r.b = put_b(bp);
     return r;
   }
-  DenOff dense(const float* w, const float* b, int cin, int cout, int cinp, int coutp) {
+  // kperm: 0 = natural K order; 32 / 16 = K permuted so that the MFMA C layout of the
+  // producing layer (lane (t,g) holds channels 16n + 4g + j (f16) / 16n + g + 4j (f64))
+  // is directly the B fragment (kernels: CFrag).
+  static int kperm_channel(int p, int kperm) {
+    if (kperm == 32) return 32 * (p / 32) + 16 * ((p % 8) / 4) + 4 * ((p % 32) / 8) + (p % 4);
+    if (kperm == 16) return 16 * (p / 16) + (p % 16) / 4 + 4 * (p % 4);
+    return p;
+  }
+  DenOff dense(const float* w, const float* b, int cin, int cout, int cinp, int coutp, int kperm = 0) {
     std::vector<WT> wp((size_t)coutp * cinp, WT(0));
     std::vector<BT> bp(coutp, BT(0));
-    for (int c = 0; c < cin; ++c)
-      for (int o = 0; o < cout; ++o) wp[(size_t)o * cinp + c] = (WT)w[(size_t)c * cout + o];
+    for (int pk = 0; pk < cinp; ++pk) {
+      const int c = kperm_channel(pk, kperm);
+      if (c >= cin) continue;
+      for (int o = 0; o < cout; ++o) wp[(size_t)o * cinp + pk] = (WT)w[(size_t)c * cout + o];
+    }
     for (int o = 0; o < cout; ++o) bp[o] = (BT)b[o];
     return DenOff{put_w(wp), put_b(bp)};
   }
@@ -191,8 +204,9 @@ int build_model(const nrx_desc* d, const float* const* w, int kc, DeviceModel<WT
     k += 3;
     return r;
   };
+  // every dense layer of the engine consumes an MFMA accumulator tile: K permuted
   auto den = [&](int cin, int cout, int cinp, int coutp) {
-    DO r = pk.dense(w[k], w[k + 1], cin, cout, cinp, coutp);
+    DO r = pk.dense(w[k], w[k + 1], cin, cout, cinp, coutp, kc);
     k += 2;
     return r;
   };
@@ -312,7 +326,7 @@ struct nrx_handle {
 
 static size_t state_bytes(const nrx_shape* s, int precision) {
   const size_t es = precision == NRX_PREC_F16 ? 2 : 4;
-  return align256((size_t)s->batch * s->num_tx * s->num_subcarriers * kTP * kDSP * es);
+  return align256((size_t)s->batch * s->num_tx * s->num_subcarriers * kT * kDS * es);
 }
 
 static int check_shape(const nrx_shape* s) {
@@ -355,7 +369,9 @@ static void fill_args(FwdArgs<WT, BT, S>& a, const nrx_handle* h, const nrx_io* 
   const size_t sb = state_bytes(s, io->precision);
   a.s_in = (S*)(p + sb);
   a.s_out = (S*)p;
-  a.a = (S*)(p + 2 * sb);
+  a.a = (S*)(p + 3 * sb);
+  a.a_out = (S*)(p + 2 * sb);
+  a.counters = (unsigned*)(p + 4 * sb);
 }
 
 
@@ -421,7 +437,9 @@ int nrx_workspace_size(const nrx_handle* h, const nrx_shape* shape, int32_t prec
   if (rc) return rc;
   if (precision != NRX_PREC_F16 && precision != NRX_PREC_F32X)
     return fail(NRX_ERR_INVALID_ARG, "unknown precision");
-  *bytes = align256((size_t)shape->batch * sizeof(double)) + 3 * state_bytes(shape, precision);
+  const int strips = (shape->num_subcarriers + strip_width(precision) - 1) / strip_width(precision);
+  *bytes = align256((size_t)shape->batch * sizeof(double)) + 4 * state_bytes(shape, precision) +
+           align256((size_t)(kMaxIt + 1) * shape->batch * strips * sizeof(unsigned));
   return NRX_OK;
 }
 

@@ -1,8 +1,8 @@
 // nrx_internal.h -- shared between the HIP kernels and the host side of libnrx.so.
 //
 // Device data layout (see DESIGN.md "Data layout in HBM"):
-//   state / aggregate buffers  s, a : [B][U][F][16][64]   (t padded 14 -> 16 with zero
-//                                     rows, channels d_s = 56 padded to 64 with zeros)
+//   state / aggregate buffers  s, a : [B][U][F][14][56]   (compact, no padding in HBM;
+//                                     the kernels pad T -> 16 and channels in LDS)
 //   storage type: _Float16 (NRX_PREC_F16) or float (NRX_PREC_F32X)
 // Packed weights (one blob per precision, built by nrx_create):
 //   separable conv: dw [9][CINP] (tap = i*3 + j, i along F, j along T),
@@ -67,14 +67,16 @@ struct FwdArgs {
   float* llr;                      // [H][B][U][F][T][bits_max]
   float* h_ref;                    // [B][U][F][T][2A] or null
   double* norm;                    // [B] workspace
-  S* s_in;                         // [B][U][F][16][64]
+  S* s_in;                         // [B][U][F][14][56]
   S* s_out;
-  S* a;
+  S* a;                            // aggregate read by this update
+  S* a_out;                        // aggregate written by the tail
+  unsigned* counters;              // [num_it + 1][B][strips] arrival tickets
 };
 
 // Optional per-kernel timing (nrx_profile_enable): events recorded around each launch on
 // the launch stream.  Kernel ids:
-enum KernelId { K_NORM = 0, K_INIT = 1, K_AGG = 2, K_UPDATE = 3, K_READOUT = 4, K_COUNT = 5 };
+enum KernelId { K_NORM = 0, K_INIT = 1, K_UPDATE = 2, K_COUNT = 3 };
 
 struct Prof {
   virtual void begin(int kid, void* stream) = 0;

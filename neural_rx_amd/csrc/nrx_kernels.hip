@@ -33,7 +33,25 @@
 
 #include "nrx_internal.h"
 
+#ifndef NRX_ABLATE
+#define NRX_ABLATE 0   // diagnostic builds only: 1 skip conv math, 2 skip z loads, 4 skip weight
+                       // staging, 8 skip tails, 16 skip conv3 global epilogue
+#endif
+
 namespace nrx {
+
+#ifdef NRX_STAMPS
+// diagnostic builds only: s_memtime per phase, wave 0 lane 0 of each workgroup
+__device__ unsigned long long g_nrx_stamps[4096][8];
+__device__ __forceinline__ void stamp(int k) {
+  if (threadIdx.x == 0) {
+    const int wg = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    if (wg < 4096) g_nrx_stamps[wg][k] = __builtin_amdgcn_s_memtime();
+  }
+}
+#else
+__device__ __forceinline__ void stamp(int) {}
+#endif
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
@@ -61,13 +79,18 @@ struct P16 {
   static constexpr int KC = 32;   // channels per K chunk (one MFMA K)
   static constexpr int CPL = 8;   // channels per lane per chunk
   static constexpr int EPC = 8;   // storage elements per 16-byte LDS chunk
-  static constexpr int FO = 12;   // output subcarriers per strip
+  static constexpr int FO = 24;   // output subcarriers per strip
+  static constexpr int R = 4;     // consecutive subcarrier rows per wave pass
+  static constexpr bool WLDS = true;  // stage each layer's weights in LDS
   __device__ static DV ld_lds(const char* p) { return *reinterpret_cast<const half8*>(p); }
   __device__ static DV ld_glb(const S* p) { return *reinterpret_cast<const half8*>(p); }
   __device__ static DV ld_w(const WT* p) { return *reinterpret_cast<const half8*>(p); }
   __device__ static Acc zero() { return Acc{0.f, 0.f, 0.f, 0.f}; }
   __device__ static Acc mma(const WT* a, DV b, Acc c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(*reinterpret_cast<const half8*>(a), b, c, 0, 0, 0);
+  }
+  __device__ static Acc mma_v(DV a, DV b, Acc c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
   }
   __device__ static int co(int g, int j) { return 4 * g + j; }
   __device__ static DV shr(DV v) {
@@ -92,7 +115,9 @@ struct P64 {
   static constexpr int KC = 16;
   static constexpr int CPL = 4;
   static constexpr int EPC = 4;
-  static constexpr int FO = 4;
+  static constexpr int FO = 8;
+  static constexpr int R = 1;
+  static constexpr bool WLDS = false;   // weights read from global (L2-resident)
   __device__ static DV ld_lds(const char* p) {
     floatx4 v = *reinterpret_cast<const floatx4*>(p);
     return DV{v[0], v[1], v[2], v[3]};
@@ -102,6 +127,13 @@ struct P64 {
   __device__ static Acc zero() { return Acc{0.0, 0.0, 0.0, 0.0}; }
   __device__ static Acc mma(const WT* a, DV b, Acc c) {
     doublex4 av = *reinterpret_cast<const doublex4*>(a);
+    c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[2], b[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[3], b[3], c, 0, 0, 0);
+    return c;
+  }
+  __device__ static Acc mma_v(DV av, DV b, Acc c) {
     c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], b[0], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1], b[1], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f64_16x16x4f64(av[2], b[2], c, 0, 0, 0);
@@ -150,42 +182,198 @@ __device__ __forceinline__ void lds_store(char* base, int off, typename P::Real 
 }
 
 // ------------------------------------------------ depthwise 3x3 + pointwise on MFMA
-// Output row `row` (buffer index in `in`, rows row-1..row+1 must exist), all COUTP
-// channels, pre-bias.  acc[n][j] = out[co = 16 n + P::co(g, j)][t].
+// Strip image in LDS: slot (one subcarrier row) x 16 symbols x up to 128 channels, with a
+// fixed slot pitch so that every layer of a block can run in place in one buffer.
+template <class P>
+constexpr int slot_pitch() { return kTP * kHID * (int)sizeof(typename P::S); }
+template <class P, int NQ>
+__device__ __forceinline__ int xoff(int slot, int t, int q) {
+  return slot * slot_pitch<P>() + (t * NQ + (q ^ swz<NQ>(t))) * 16;
+}
+
+// Per-layer weight image in LDS (P16): W^T [COUTP][CINP] as 16-row tiles addressed like an
+// activation image (co>>4, co&15, chunk), then dw [9][CINP], then bias [COUTP] (f32).
+constexpr int kWPw = kHID * kHID * 2;          // 32 KB
+constexpr int kWDw = 9 * kHID * 2;             // 2304 B
+constexpr int kWBias = kWPw + kWDw;            // conv bias [COUTP] f32
+constexpr int kWTailBias = kWBias + kHID * 4;  // aggregation-MLP biases (2 x 64 f32)
+constexpr int kWBytes = kWTailBias + 2 * kAGG * 4;
+
 template <class P, int CINP, int COUTP>
-__device__ __forceinline__ void sep_tile(const char* in, int row, int t, int g, int lane,
-                                         const SepW<typename P::WT, typename P::BT>& w,
-                                         typename P::Acc (&acc)[COUTP / 16]) {
+struct WLds {
+  const char* base;
+  static constexpr int NQ = CINP * 2 / 16;
+  __device__ typename P::DV afrag(int n, int kc, int lane, int g) const {
+    return *reinterpret_cast<const half8*>(base + lds_off<NQ>(n, lane & 15, kc * 4 + g));
+  }
+  __device__ typename P::DV dwv(int tap, int kc, int g) const {
+    return *reinterpret_cast<const half8*>(base + kWPw + (tap * CINP + kc * 32 + g * 8) * 2);
+  }
+  __device__ float bias(int co) const { return reinterpret_cast<const float*>(base + kWBias)[co]; }
+};
+
+template <class P, int CINP, int COUTP>
+struct WGlb {
+  SepW<typename P::WT, typename P::BT> w;
+  __device__ typename P::DV afrag(int n, int kc, int lane, int g) const {
+    return P::ld_w(w.pw + (16 * n + (lane & 15)) * CINP + kc * P::KC + g * P::CPL);
+  }
+  __device__ typename P::DV dwv(int tap, int kc, int g) const {
+    return P::ld_w(w.dw + tap * CINP + kc * P::KC + g * P::CPL);
+  }
+  __device__ typename P::BT bias(int co) const { return w.b[co]; }
+};
+
+// Cooperative copy of one separable layer's packed weights into the LDS image.  All
+// global loads of a thread are issued before any LDS store (a load -> wait -> store loop
+// would pay one full memory latency per chunk).
+template <int CINP, int COUTP>
+__device__ __forceinline__ void stage_weights(char* wb, const SepW<_Float16, float>& w) {
+  constexpr int NQ = CINP * 2 / 16;
+  constexpr int NPW = COUTP * NQ;                 // W^T chunks
+  constexpr int NDW = 9 * NQ;                     // dw chunks
+  constexpr int NB = COUTP / 4;                   // bias chunks (4 floats)
+  constexpr int NT = 512;
+  constexpr int PER = (NPW + NT - 1) / NT;
+  const int tid = threadIdx.x;
+  intx4 v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int idx = tid + i * NT;
+    if (idx < NPW) {
+      const int co = idx / NQ, q = idx % NQ;
+      v[i] = *reinterpret_cast<const intx4*>(w.pw + co * CINP + q * 8);
+    }
+  }
+  intx4 vd = {0, 0, 0, 0}, vb = {0, 0, 0, 0};
+  if (tid < NDW) vd = reinterpret_cast<const intx4*>(w.dw)[tid];
+  else if (tid - NDW < NB) vb = reinterpret_cast<const intx4*>(w.b)[tid - NDW];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int idx = tid + i * NT;
+    if (idx < NPW) {
+      const int co = idx / NQ, q = idx % NQ;
+      *reinterpret_cast<intx4*>(wb + lds_off<NQ>(co >> 4, co & 15, q)) = v[i];
+    }
+  }
+  if (tid < NDW) reinterpret_cast<intx4*>(wb + kWPw)[tid] = vd;
+  else if (tid - NDW < NB) reinterpret_cast<intx4*>(wb + kWPw + kWDw)[tid - NDW] = vb;
+}
+
+// R consecutive output rows (input slots s0 .. s0+R-1, neighbours s0-1 and s0+R) of one
+// wave, all COUTP channels, pre-bias.  acc[r][n][j] = out[row r][co = 16 n + P::co(g,j)][t].
+// The depthwise weights and every pointwise A fragment are loaded once per K chunk and
+// reused over the R rows; the three input rows of consecutive outputs overlap, so a pass
+// reads R + 2 activation rows instead of 3 R.
+template <class P, int CINP, int COUTP, class WS>
+__device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int t, int g, int lane,
+                                          const WS& ws,
+                                          typename P::Acc (&acc)[P::R][COUTP / 16]) {
   using DV = typename P::DV;
+  constexpr int R = P::R;
   constexpr int NQ = CINP * (int)sizeof(typename P::S) / 16;
   constexpr int NKC = CINP / P::KC;
 #pragma unroll
-  for (int n = 0; n < COUTP / 16; ++n) acc[n] = P::zero();
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int n = 0; n < COUTP / 16; ++n) acc[r][n] = P::zero();
   const int sw = swz<NQ>(t);
-  const char* rm = in + ((row - 1) * kTP + t) * NQ * 16;
-  const char* r0 = rm + kTP * NQ * 16;
-  const char* rp = r0 + kTP * NQ * 16;
-  const typename P::WT* pwrow = w.pw + (lane & 15) * CINP + g * P::CPL;
-#pragma unroll 2
+  int rb[R + 2];
+#pragma unroll
+  for (int i = 0; i < R + 2; ++i) {
+    int sl = s0 - 1 + i;
+    sl = sl < 0 ? 0 : (sl >= nslots ? nslots - 1 : sl);
+    rb[i] = sl * slot_pitch<P>() + t * NQ * 16;
+  }
   for (int kc = 0; kc < NKC; ++kc) {
     const int off = ((kc * 4 + g) ^ sw) * 16;
-    const DV xm = P::ld_lds(rm + off);
-    const DV x0 = P::ld_lds(r0 + off);
-    const DV xp = P::ld_lds(rp + off);
-    const typename P::WT* dw = w.dw + kc * P::KC + g * P::CPL;
-    const DV w0 = P::ld_w(dw + 0 * CINP), w1 = P::ld_w(dw + 1 * CINP), w2 = P::ld_w(dw + 2 * CINP);
-    const DV w3 = P::ld_w(dw + 3 * CINP), w4 = P::ld_w(dw + 4 * CINP), w5 = P::ld_w(dw + 5 * CINP);
-    const DV w6 = P::ld_w(dw + 6 * CINP), w7 = P::ld_w(dw + 7 * CINP), w8 = P::ld_w(dw + 8 * CINP);
-    // column sums per symbol offset dt = j - 1 (tap = i*3 + j, i along subcarriers)
-    const DV cm = w0 * xm + w3 * x0 + w6 * xp;
-    const DV c0 = w1 * xm + w4 * x0 + w7 * xp;
-    const DV cp = w2 * xm + w5 * x0 + w8 * xp;
-    const DV d = c0 + P::shr(cm) + P::shl(cp);
+    DV xs[R + 2];
 #pragma unroll
-    for (int n = 0; n < COUTP / 16; ++n)
-      acc[n] = P::mma(pwrow + n * 16 * CINP + kc * P::KC, d, acc[n]);
+    for (int i = 0; i < R + 2; ++i) xs[i] = P::ld_lds(X + rb[i] + off);
+    DV w[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) w[k] = ws.dwv(k, kc, g);
+    DV d[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      // column sums per symbol offset dt = j - 1 (tap = i*3 + j, i along subcarriers)
+      const DV cm = w[0] * xs[r] + w[3] * xs[r + 1] + w[6] * xs[r + 2];
+      const DV c0 = w[1] * xs[r] + w[4] * xs[r + 1] + w[7] * xs[r + 2];
+      const DV cp = w[2] * xs[r] + w[5] * xs[r + 1] + w[8] * xs[r + 2];
+      d[r] = c0 + P::shr(cm) + P::shl(cp);
+    }
+#pragma unroll
+    for (int n = 0; n < COUTP / 16; ++n) {
+      const DV a = ws.afrag(n, kc, lane, g);
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r][n] = P::mma_v(a, d[r], acc[r][n]);
+    }
   }
 }
+
+// One layer over output positions [pos_lo, pos_hi) in rounds of 8 waves x R rows.  Every
+// round computes into registers, then (after a barrier) hands the accumulators to `epi`,
+// which may overwrite input slots of rows this round consumed (in-place layers: the
+// output of position p goes to slot p - in_off - 1, which no later round reads).
+template <class P, int CINP, int COUTP, class WS, class Epi>
+__device__ __forceinline__ void conv_layer(const char* X, int nslots, int in_off, int pos_lo,
+                                           int pos_hi, const WS& ws, Epi&& epi) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int t = lane & 15, g = lane >> 4;
+  for (int base = pos_lo; base < pos_hi; base += 8 * P::R) {
+    const int p0 = base + wave * P::R;
+    const bool act = p0 < pos_hi;
+    typename P::Acc acc[P::R][COUTP / 16];
+    if (act) {
+      if constexpr (NRX_ABLATE & 1) {
+#pragma unroll
+        for (int r = 0; r < P::R; ++r)
+#pragma unroll
+          for (int n = 0; n < COUTP / 16; ++n) acc[r][n] = P::zero();
+      } else {
+        conv_rows<P, CINP, COUTP>(X, p0 - in_off, nslots, t, g, lane, ws, acc);
+      }
+    }
+    __syncthreads();
+    epi.pre();                       // all threads (e.g. stage tail weights into X)
+    if (act) epi(acc, p0, t, g);
+    __syncthreads();
+  }
+}
+
+// In-place epilogue: +bias, ReLU, zero outside the grid / t >= 14, store to slot p-in_off-1.
+template <class P, int COUTP, class WS>
+struct EpiInPlace {
+  char* X;
+  int in_off, pos_hi, f_start, F;
+  WS ws;
+  __device__ void pre() const {}
+  __device__ void operator()(const typename P::Acc (&acc)[P::R][COUTP / 16], int p0, int t, int g) const {
+    using Real = typename P::Real;
+    constexpr int NQ = COUTP * (int)sizeof(typename P::S) / 16;
+#pragma unroll
+    for (int r = 0; r < P::R; ++r) {
+      const int p = p0 + r;
+      if (p >= pos_hi) continue;
+      const int f = f_start + p;
+      const bool z = f < 0 || f >= F || t >= kT;
+      const int slot = p - in_off - 1;
+#pragma unroll
+      for (int n = 0; n < COUTP / 16; ++n) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int co = 16 * n + P::co(g, j);
+          Real v = (Real)acc[r][n][j] + (Real)ws.bias(co);
+          v = v > (Real)0 ? v : (Real)0;
+          if (z) v = (Real)0;
+          *reinterpret_cast<typename P::S*>(X + xoff<P, NQ>(slot, t, co / P::EPC) +
+                                            (co % P::EPC) * (int)sizeof(typename P::S)) =
+              (typename P::S)v;
+        }
+      }
+    }
+  }
+};
 
 // Dense layer on one 16-row tile with the B operand from a 16-byte-chunk source.
 template <class P, int CINP, int COUTP, class Src>
@@ -261,340 +449,589 @@ __global__ __launch_bounds__(256) void k_norm(const float* __restrict__ y, int n
   }
 }
 
-// ===================================================== separable-conv strip kernels
+// ===================================================== separable-conv block kernels
+// One workgroup = one (slot, user, subcarrier strip) running the 3-conv block of the
+// state init or of one iteration's state update.  The per-user MLPs that consume the new
+// state run in the conv3 epilogue straight from the accumulators: the MFMA C layout of a
+// 16-channel tile (lane (t, g) holds channels 16 n + P::co(g, j)) is reused as the B
+// operand of the next MFMA, with that layer's K axis permuted on the host to match
+// (nrx_api.cpp, kperm_*).  After an update that is not the last, the epilogue applies
+// the aggregation MLP of the next iteration and stores act_u * sp_u; the last workgroup
+// of each (slot, strip) to arrive then forms the leave-one-out mean for all users.  After
+// the last update the epilogue runs the LLR / ChEst readouts instead.
+//
+// State / aggregate buffers are compact: [B][U][F][14][56] (no padding in HBM).
+
+enum Tail { TAIL_NONE = -1, TAIL_AGG = 0, TAIL_READOUT = 1 };
+
 template <class P>
-struct InitParams {
+struct BlockParams {
   FwdArgs<typename P::WT, typename P::BT, typename P::S> a;
-  SepW<typename P::WT, typename P::BT> w[kMaxInit][3];
+  SepW<typename P::WT, typename P::BT> w[3];             // the block's separable layers
+  DenseW<typename P::WT, typename P::BT> agg[2];         // next iteration's aggregation MLP
+  DenseW<typename P::WT, typename P::BT> llr[kMaxHeads][2];
+  DenseW<typename P::WT, typename P::BT> chest[2];
+  int tail;                                              // TAIL_AGG / TAIL_READOUT / TAIL_NONE
+  int m;                                                 // init: which StateInit (Var-IO)
+  unsigned* counters;                                    // [B][strips] arrival tickets (agg tail)
 };
 
 template <class P>
-struct UpdParams {
-  FwdArgs<typename P::WT, typename P::BT, typename P::S> a;
-  SepW<typename P::WT, typename P::BT> w[3];
-};
-
+constexpr int strip_slots() { return P::FO + 2 * kHalo; }
 template <class P>
-constexpr int strip_lds_bytes(int cinp0) {
-  // X: FO+6 rows of max(cinp0, 128) channels; Y: FO+4 rows of 128 channels
-  return (P::FO + 2 * kHalo) * kTP * (cinp0 > kHID ? cinp0 : kHID) * (int)sizeof(typename P::S) +
-         (P::FO + 2 * kHalo - 2) * kTP * kHID * (int)sizeof(typename P::S);
+constexpr int strip_lds_bytes() {
+  return strip_slots<P>() * slot_pitch<P>() + (P::WLDS ? kWBytes : 0);
+}
+static_assert(P16::FO <= 8 * P16::R, "the conv3 of a strip must run in one round");
+
+__device__ __forceinline__ size_t srow(int b, int u, int f, int t, int U, int F) {
+  return ((((size_t)b * U + u) * F + f) * kT + t) * kDS;
 }
 
-// conv1 (X rows [1,R0-1) -> Y rows shifted by 1) and conv2 (Y -> X rows [2,R0-2)).
+// Runs one separable layer of a block over the strip: stage weights (P16), then
+// conv_layer with the given epilogue.  `extra_stage` runs with the weight staging.
+template <class P, int CINP, int COUTP, class Epi, class Extra>
+__device__ __forceinline__ void strip_layer(char* X, char* WB, const SepW<typename P::WT, typename P::BT>& w,
+                                            int in_off, int pos_lo, int pos_hi, Epi&& epi_of,
+                                            Extra&& extra_stage) {
+  constexpr int R0 = strip_slots<P>();
+  if constexpr (P::WLDS) {
+    if constexpr (!(NRX_ABLATE & 4)) stage_weights<CINP, COUTP>(WB, w);
+    extra_stage();
+    __syncthreads();
+    WLds<P, CINP, COUTP> ws{WB};
+    conv_layer<P, CINP, COUTP>(X, R0, in_off, pos_lo, pos_hi, ws, epi_of(ws));
+  } else {
+    WGlb<P, CINP, COUTP> ws{w};
+    conv_layer<P, CINP, COUTP>(X, R0, in_off, pos_lo, pos_hi, ws, epi_of(ws));
+  }
+}
+
+struct NoStage {
+  __device__ void operator()() const {}
+};
+
+// conv1 + conv2 of a block, in place: positions p in [1, R0-1) then [2, R0-2).
 template <class P, int CINP>
-__device__ __forceinline__ void strip_conv12(char* X, char* Y, int f_start, int F,
+__device__ __forceinline__ void strip_conv12(char* X, char* WB, int f_start, int F,
                                              const SepW<typename P::WT, typename P::BT>* w) {
-  constexpr int R0 = P::FO + 2 * kHalo;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int t = lane & 15, g = lane >> 4;
-  typename P::Acc acc[kHID / 16];
-  for (int lf = 1 + wave; lf < R0 - 1; lf += 8) {
-    const int f = f_start + lf;
-    const bool valid = f >= 0 && f < F;
-    if (valid) sep_tile<P, CINP, kHID>(X, lf, t, g, lane, w[0], acc);
-    else {
-#pragma unroll
-      for (int n = 0; n < kHID / 16; ++n) acc[n] = P::zero();
-    }
-    epi_lds<P, kHID>(Y, lf - 1, t, g, acc, w[0].b, true, !valid);
-  }
-  __syncthreads();
-  for (int lf = 2 + wave; lf < R0 - 2; lf += 8) {
-    const int f = f_start + lf;
-    const bool valid = f >= 0 && f < F;
-    if (valid) sep_tile<P, kHID, kHID>(Y, lf - 1, t, g, lane, w[1], acc);
-    else {
-#pragma unroll
-      for (int n = 0; n < kHID / 16; ++n) acc[n] = P::zero();
-    }
-    epi_lds<P, kHID>(X, lf, t, g, acc, w[1].b, true, !valid);
-  }
-  __syncthreads();
+  constexpr int R0 = strip_slots<P>();
+  strip_layer<P, CINP, kHID>(X, WB, w[0], 0, 1, R0 - 1, [&](auto ws) {
+    return EpiInPlace<P, kHID, decltype(ws)>{X, 0, R0 - 1, f_start, F, ws};
+  }, NoStage{});
+  stamp(2);
+  strip_layer<P, kHID, kHID>(X, WB, w[1], 1, 2, R0 - 2, [&](auto ws) {
+    return EpiInPlace<P, kHID, decltype(ws)>{X, 1, R0 - 2, f_start, F, ws};
+  }, NoStage{});
 }
 
-// StateInit (+ Var-IO mix).  grid = (strips, U, B), block = 512.
+// ------------------------------------------------------ dense layers from registers
+// Dense weights: LDS image (P16, staged by the workgroup) or global (P64); K permuted.
 template <class P, int CINP>
-__global__ __launch_bounds__(512) void k_init(InitParams<P> prm) {
+struct DLds {
+  const char* base;
+  const float* bias_p;
+  static constexpr int NQ = CINP * 2 / 16;
+  __device__ typename P::DV afrag(int n, int kc, int lane, int g) const {
+    return *reinterpret_cast<const half8*>(base + lds_off<NQ>(n, lane & 15, kc * 4 + g));
+  }
+  __device__ float bias(int co) const { return bias_p[co]; }
+};
+template <class P, int CINP>
+struct DGlb {
+  DenseW<typename P::WT, typename P::BT> w;
+  __device__ typename P::DV afrag(int n, int kc, int lane, int g) const {
+    return P::ld_w(w.w + (16 * n + (lane & 15)) * CINP + kc * P::KC + g * P::CPL);
+  }
+  __device__ typename P::BT bias(int co) const { return w.b[co]; }
+};
+
+// Stage a dense layer (P16) at `dst` (W^T image, K permuted on the host) and its bias at
+// `bias_dst`.
+template <int CINP, int COUTP>
+__device__ __forceinline__ void stage_dense(char* dst, float* bias_dst, const DenseW<_Float16, float>& w) {
+  constexpr int NQ = CINP * 2 / 16;
+  constexpr int NW = COUTP * NQ;
+  for (int idx = threadIdx.x; idx < NW; idx += 512) {
+    const int co = idx / NQ, q = idx % NQ;
+    *reinterpret_cast<intx4*>(dst + lds_off<NQ>(co >> 4, co & 15, q)) =
+        *reinterpret_cast<const intx4*>(w.w + co * CINP + q * 8);
+  }
+  for (int idx = threadIdx.x; idx < COUTP; idx += 512) bias_dst[idx] = w.b[idx];
+}
+
+// B fragments of a dense layer whose input is NT accumulator tiles in C layout.
+template <class P, int NT>
+struct CFrag {
+  static constexpr int NKC = NT * 16 / P::KC;
+  typename P::DV b[NKC];
+  __device__ CFrag(const typename P::Real (&v)[NT][4]) {
+    if constexpr (P::KC == 32) {
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc)
+        b[kc] = typename P::DV{(_Float16)v[2 * kc][0], (_Float16)v[2 * kc][1], (_Float16)v[2 * kc][2],
+                               (_Float16)v[2 * kc][3], (_Float16)v[2 * kc + 1][0], (_Float16)v[2 * kc + 1][1],
+                               (_Float16)v[2 * kc + 1][2], (_Float16)v[2 * kc + 1][3]};
+    } else {
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc)
+        b[kc] = typename P::DV{(double)v[kc][0], (double)v[kc][1], (double)v[kc][2], (double)v[kc][3]};
+    }
+  }
+};
+
+template <class P, int NT, int COUTP, class WS>
+__device__ __forceinline__ void dense_c(const CFrag<P, NT>& in, const WS& ws, int lane, int g,
+                                        typename P::Real (&out)[COUTP / 16][4], bool relu) {
+  using Real = typename P::Real;
+#pragma unroll
+  for (int n = 0; n < COUTP / 16; ++n) {
+    typename P::Acc acc = P::zero();
+#pragma unroll
+    for (int kc = 0; kc < CFrag<P, NT>::NKC; ++kc) acc = P::mma_v(ws.afrag(n, kc, lane, g), in.b[kc], acc);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      Real v = (Real)acc[j] + (Real)ws.bias(16 * n + P::co(g, j));
+      out[n][j] = relu ? (v > (Real)0 ? v : (Real)0) : v;
+    }
+  }
+}
+
+// Readout weight images staged into the (then free) strip buffer X (P16).
+constexpr int kHeadSlot = 24 * 1024;   // W1^T 16 KB | W2^T <= 8 KB ... per head, 256-aligned
+__device__ __forceinline__ int head_w1(int h) { return h * (kHeadSlot + 1024); }
+__device__ __forceinline__ int head_w2(int h) { return head_w1(h) + 16 * 1024; }
+__device__ __forceinline__ int head_b1(int h) { return head_w1(h) + kHeadSlot; }
+__device__ __forceinline__ int head_b2(int h) { return head_b1(h) + 512; }
+
+// conv3 epilogue: new state rows (+ aggregation MLP or readouts) for R rows of a wave.
+template <class P, class WS, int CHP, int TAILM>
+struct EpiConv3 {
   using S = typename P::S;
   using Real = typename P::Real;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int R0 = P::FO + 2 * kHalo;
+  const BlockParams<P>* prm;
+  char* X;
+  char* WB;
+  WS ws;
+  int b, u, f_start, pos_hi, mode;   // mode 0: update (+skip), 1: init (x wm, Var-IO accumulate)
+  Real wm;
+  bool first;
+
+  __device__ void pre() const {
+    if constexpr (P::WLDS) {
+      if constexpr (TAILM == TAIL_READOUT) {
+        // stage the readout heads into X (every wave is past its conv3 reads)
+        const auto& a = prm->a;
+        for (int h = 0; h <= a.H; ++h) {
+          const bool ch = h == a.H;
+          const DenseW<_Float16, float>* d = ch ? prm->chest : prm->llr[h];
+          stage_dense<kDSP, kHID>(X + head_w1(h), reinterpret_cast<float*>(X + head_b1(h)), d[0]);
+          if (ch) stage_dense<kHID, CHP>(X + head_w2(h), reinterpret_cast<float*>(X + head_b2(h)), d[1]);
+          else stage_dense<kHID, 16>(X + head_w2(h), reinterpret_cast<float*>(X + head_b2(h)), d[1]);
+        }
+        __syncthreads();
+      }
+    }
+  }
+
+  template <int NH2, class W1, class W2>
+  __device__ __forceinline__ void head(const CFrag<P, kDSP / 16>& sb, const W1& w1, const W2& w2, int lane,
+                                       int g, Real (&o)[NH2][4]) const {
+    Real hdn[kHID / 16][4];
+    dense_c<P, kDSP / 16, kHID>(sb, w1, lane, g, hdn, true);
+    CFrag<P, kHID / 16> hb(hdn);
+    dense_c<P, kHID / 16, NH2 * 16>(hb, w2, lane, g, o, false);
+  }
+
+  __device__ void operator()(const typename P::Acc (&acc)[P::R][kDSP / 16], int p0, int t, int g) const {
+    const auto& a = prm->a;
+    const int F = a.F, U = a.U;
+    const int lane = threadIdx.x & 63;
+    const bool tv = t < kT && !(NRX_ABLATE & 16);
+#pragma unroll
+    for (int r = 0; r < P::R; ++r) {
+      const int p = p0 + r;
+      const int f = f_start + p;
+      if (p >= pos_hi || f >= F) continue;     // wave-uniform
+      const size_t off = srow(b, u, f, tv ? t : 0, U, F);
+      // ---- new state s (C layout, channels >= 56 forced to 0)
+      Real sv[kDSP / 16][4];
+#pragma unroll
+      for (int n = 0; n < kDSP / 16; ++n) {
+        Real prev[4] = {0, 0, 0, 0};
+        const int c0 = 16 * n + P::co(g, 0);
+        if (tv && (mode == 0 || !first)) {
+          const S* src = (mode == 0 ? a.s_in : a.s_out) + off;
+          if constexpr (sizeof(S) == 2) {
+            if (c0 < kDS) {
+              const half4 h4 = *reinterpret_cast<const half4*>(src + c0);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) prev[j] = (Real)h4[j];
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int co = 16 * n + P::co(g, j);
+              if (co < kDS) prev[j] = (Real)src[co];
+            }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int co = 16 * n + P::co(g, j);
+          Real v = (Real)acc[r][n][j] + (Real)ws.bias(co);
+          if (mode == 1) v *= wm;
+          v += prev[j];
+          if (co >= kDS) v = 0;
+          sv[n][j] = (Real)(S)v;               // the state is stored (and consumed) in S
+        }
+      }
+      if (TAILM != TAIL_READOUT && tv) {
+        S* dst = a.s_out + off;
+        if constexpr (sizeof(S) == 2) {
+#pragma unroll
+          for (int n = 0; n < kDSP / 16; ++n) {
+            const int c0 = 16 * n + 4 * g;
+            if (c0 < kDS)
+              *reinterpret_cast<half4*>(dst + c0) =
+                  half4{(S)sv[n][0], (S)sv[n][1], (S)sv[n][2], (S)sv[n][3]};
+          }
+        } else {
+#pragma unroll
+          for (int n = 0; n < kDSP / 16; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int co = 16 * n + P::co(g, j);
+              if (co < kDS) dst[co] = (S)sv[n][j];
+            }
+        }
+      }
+      if constexpr (TAILM == TAIL_NONE) continue;
+      CFrag<P, kDSP / 16> sb(sv);
+      if constexpr (TAILM == TAIL_AGG) {
+        // sp_u = act_u * (W2 relu(W1 s + b1) + b2)  -> a_out (combined by the tail)
+        Real hdn[kAGG / 16][4], sp[kDSP / 16][4];
+        const Real act = (Real)a.active[(size_t)b * U + u];
+        if constexpr (P::WLDS) {
+          DLds<P, kDSP> w1{WB + 16 * 1024, reinterpret_cast<const float*>(WB + kWTailBias)};
+          DLds<P, kAGG> w2{WB + 24 * 1024, reinterpret_cast<const float*>(WB + kWTailBias + kAGG * 4)};
+          dense_c<P, kDSP / 16, kAGG>(sb, w1, lane, g, hdn, true);
+          CFrag<P, kAGG / 16> hb(hdn);
+          dense_c<P, kAGG / 16, kDSP>(hb, w2, lane, g, sp, false);
+        } else {
+          dense_c<P, kDSP / 16, kAGG>(sb, DGlb<P, kDSP>{prm->agg[0]}, lane, g, hdn, true);
+          CFrag<P, kAGG / 16> hb(hdn);
+          dense_c<P, kAGG / 16, kDSP>(hb, DGlb<P, kAGG>{prm->agg[1]}, lane, g, sp, false);
+        }
+        if (tv) {
+          S* dst = a.a_out + off;
+#pragma unroll
+          for (int n = 0; n < kDSP / 16; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int co = 16 * n + P::co(g, j);
+              if (co < kDS) dst[co] = (S)(sp[n][j] * act);
+            }
+        }
+      } else {
+        // readouts: LLR head(s) then ChEst
+        for (int hh = 0; hh <= a.H; ++hh) {
+          const bool ch = hh == a.H;
+          if (ch && !a.h_ref) break;
+          if (!ch) {
+            Real o[1][4];
+            if constexpr (P::WLDS) {
+              head<1>(sb, DLds<P, kDSP>{X + head_w1(hh), reinterpret_cast<const float*>(X + head_b1(hh))},
+                      DLds<P, kHID>{X + head_w2(hh), reinterpret_cast<const float*>(X + head_b2(hh))}, lane, g, o);
+            } else {
+              head<1>(sb, DGlb<P, kDSP>{prm->llr[hh][0]}, DGlb<P, kHID>{prm->llr[hh][1]}, lane, g, o);
+            }
+            if (tv) {
+              float* dst = a.llr + ((((size_t)hh * a.B + b) * U + u) * F + f) * kT * a.bits_max + t * a.bits_max;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const int co = P::co(g, j);
+                if (co < a.bits_max) dst[co] = co < a.head_bits[hh] ? (float)o[0][j] : 0.f;
+              }
+            }
+          } else {
+            Real o[CHP / 16][4];
+            if constexpr (P::WLDS) {
+              head<CHP / 16>(sb, DLds<P, kDSP>{X + head_w1(hh), reinterpret_cast<const float*>(X + head_b1(hh))},
+                             DLds<P, kHID>{X + head_w2(hh), reinterpret_cast<const float*>(X + head_b2(hh))}, lane,
+                             g, o);
+            } else {
+              head<CHP / 16>(sb, DGlb<P, kDSP>{prm->chest[0]}, DGlb<P, kHID>{prm->chest[1]}, lane, g, o);
+            }
+            if (tv) {
+              const int A2 = 2 * a.A;
+              float* dst = a.h_ref + ((((size_t)b * U + u) * F + f) * kT + t) * A2;
+#pragma unroll
+              for (int n = 0; n < CHP / 16; ++n)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                  const int co = 16 * n + P::co(g, j);
+                  if (co < A2) dst[co] = (float)o[n][j];
+                }
+            }
+          }
+        }
+      }
+    }
+  }
+};
+
+// conv3 (positions [3, R0-3)) with the fused epilogue; stages the aggregation MLP with
+// the conv3 weights (P16: W1^T at WB+16K, W2^T at WB+24K, biases in the tail-bias area).
+template <class P, int CHP, int TAILM>
+__device__ __forceinline__ void strip_conv3(const BlockParams<P>& prm, char* X, char* WB, int b, int u,
+                                            int f_start, int mode, typename P::Real wm, bool first) {
+  constexpr int R0 = strip_slots<P>();
+  auto extra = [&]() {
+    if constexpr (P::WLDS) {
+      if constexpr (TAILM == TAIL_AGG) {
+        stage_dense<kDSP, kAGG>(WB + 16 * 1024, reinterpret_cast<float*>(WB + kWTailBias), prm.agg[0]);
+        stage_dense<kAGG, kDSP>(WB + 24 * 1024, reinterpret_cast<float*>(WB + kWTailBias + kAGG * 4), prm.agg[1]);
+      }
+    }
+  };
+  strip_layer<P, kHID, kDSP>(X, WB, prm.w[2], 2, kHalo, R0 - kHalo, [&](auto ws) {
+    return EpiConv3<P, decltype(ws), CHP, TAILM>{&prm, X, WB, ws, b, u, f_start, R0 - kHalo, mode, wm, first};
+  }, extra);
+}
+
+// ---------------------------------------------------------------- per-user block bodies
+// StateInit_m of user u on the strip (z = [y*ns, pe, h*ns]).
+template <class P, int CINP, int CHP, int TAILM>
+__device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem, int b, int u,
+                                          int strip, typename P::Real wm, bool first) {
+  using S = typename P::S;
+  using Real = typename P::Real;
+  constexpr int R0 = strip_slots<P>();
+  constexpr int NQZ = CINP * (int)sizeof(S) / 16;
   const auto& a = prm.a;
-  const int strip = blockIdx.x, u = blockIdx.y, b = blockIdx.z;
   const int F = a.F, U = a.U, A2 = 2 * a.A;
   const int f0 = strip * P::FO;
   const int f_start = f0 - kHalo;
   char* X = smem;
-  char* Y = smem + R0 * kTP * (CINP > kHID ? CINP : kHID) * (int)sizeof(S);
+  char* WB = smem + R0 * slot_pitch<P>();
   const Real ns = (Real)a.norm[b];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int t = lane & 15, g = lane >> 4;
-  bool wrote = false;
-  for (int m = 0; m < a.num_init; ++m) {
-    Real wm = (Real)1;
-    if (!a.masking) {
-      wm = a.mcs_mask ? (Real)a.mcs_mask[((size_t)b * U + u) * a.M + m] : (Real)(m == 0 ? 1 : 0);
-      if (wm == (Real)0) continue;   // exact: contributes 0 * finite
-    }
-    // z = [y*ns (2A), pe (2), h*ns (2A), 0...] on rows [0,R0) x 16
-    for (int idx = threadIdx.x; idx < R0 * kTP * CINP; idx += 512) {
-      const int c = idx % CINP;
-      const int tt = (idx / CINP) % kTP;
-      const int lf = idx / (CINP * kTP);
-      const int f = f_start + lf;
-      Real v = 0;
-      if (f >= 0 && f < F && tt < kT) {
-        if (c < A2) v = (Real)a.y[(((size_t)b * F + f) * kT + tt) * A2 + c] * ns;
-        else if (c < A2 + 2) v = (Real)a.pe[(((size_t)u * F + f) * kT + tt) * 2 + (c - A2)];
-        else if (a.use_h && c < 2 * A2 + 2)
-          v = (Real)a.h_hat[((((size_t)b * U + u) * F + f) * kT + tt) * A2 + (c - A2 - 2)] * ns;
-      }
-      lds_store<P>(X, lds_elem_off<P, CINP>(lf, tt, c), v);
-    }
-    __syncthreads();
-    strip_conv12<P, CINP>(X, Y, f_start, F, prm.w[m]);
-    // conv3: X rows [3, R0-3) -> global s (d_s channels, padded to 64)
-    typename P::Acc acc[kDSP / 16];
-    for (int lf = kHalo + wave; lf < R0 - kHalo; lf += 8) {
-      const int f = f_start + lf;
-      if (f >= F) continue;
-      sep_tile<P, kHID, kDSP>(X, lf, t, g, lane, prm.w[m][2], acc);
-      S* dst = a.s_out + ((((size_t)b * U + u) * F + f) * kTP + t) * kDSP;
+  constexpr int NZ = R0 * kTP * CINP;
+  constexpr int BATCH = 32;
+  for (int base = 0; base < NZ; base += 512 * BATCH) {
+    Real v[BATCH];
 #pragma unroll
-      for (int n = 0; n < kDSP / 16; ++n) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int co = 16 * n + P::co(g, j);
-          Real v = ((Real)acc[n][j] + (Real)prm.w[m][2].b[co]) * wm;
-          if (wrote) v += (Real)dst[co];
-          if (t >= kT || co >= kDS) v = 0;
-          dst[co] = (S)v;
+    for (int i = 0; i < BATCH; ++i) {
+      const int idx = base + threadIdx.x + i * 512;
+      v[i] = 0;
+      if (idx < NZ) {
+        const int c = idx % CINP;
+        const int tt = (idx / CINP) % kTP;
+        const int lf = idx / (CINP * kTP);
+        const int f = f_start + lf;
+        if (f >= 0 && f < F && tt < kT) {
+          if (c < A2) v[i] = (Real)a.y[(((size_t)b * F + f) * kT + tt) * A2 + c];
+          else if (c < A2 + 2) v[i] = (Real)a.pe[(((size_t)u * F + f) * kT + tt) * 2 + (c - A2)];
+          else if (a.use_h && c < 2 * A2 + 2)
+            v[i] = (Real)a.h_hat[((((size_t)b * U + u) * F + f) * kT + tt) * A2 + (c - A2 - 2)];
         }
       }
     }
-    wrote = true;
-    __syncthreads();
-  }
-  if (!wrote) {
-    for (int idx = threadIdx.x; idx < P::FO * kTP * kDSP; idx += 512) {
-      const int f = f0 + idx / (kTP * kDSP);
-      if (f < F) a.s_out[(((size_t)b * U + u) * F + f0) * kTP * kDSP + idx] = (S)0;
+#pragma unroll
+    for (int i = 0; i < BATCH; ++i) {
+      const int idx = base + threadIdx.x + i * 512;
+      if (idx < NZ) {
+        const int c = idx % CINP;
+        const int tt = (idx / CINP) % kTP;
+        const int lf = idx / (CINP * kTP);
+        const Real sc = (c < A2 || (c >= A2 + 2 && c < 2 * A2 + 2)) ? ns : (Real)1;
+        *reinterpret_cast<S*>(X + xoff<P, NQZ>(lf, tt, c / P::EPC) + (c % P::EPC) * (int)sizeof(S)) =
+            (S)(v[i] * sc);
+      }
     }
   }
+  __syncthreads();
+  strip_conv12<P, CINP>(X, WB, f_start, F, prm.w);
+  strip_conv3<P, CHP, TAILM>(prm, X, WB, b, u, f_start, 1, wm, first);
 }
 
-// UpdateState: z = [a, s, pe] -> 3 sep convs + skip.  grid = (strips, U, B), block 512.
-template <class P>
-__global__ __launch_bounds__(512) void k_update(UpdParams<P> prm) {
+// UpdateState of user u on the strip (z = [a, s, pe]).
+template <class P, int CHP, int TAILM>
+__device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* smem, int b, int u, int strip) {
   using S = typename P::S;
-  using Real = typename P::Real;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int R0 = P::FO + 2 * kHalo;
-  constexpr int CINP = kUPD_CINP;
-  constexpr int NQ = CINP * (int)sizeof(S) / 16;      // chunks per z row
-  constexpr int QS = kDS / P::EPC;                     // chunks of a (and of s) in z
+  constexpr int R0 = strip_slots<P>();
+  constexpr int NQ = kUPD_CINP * (int)sizeof(S) / 16;  // chunks per z row
+  constexpr int QS = kDS / P::EPC;                      // chunks of a (and of s) in z
   const auto& a = prm.a;
-  const int strip = blockIdx.x, u = blockIdx.y, b = blockIdx.z;
   const int F = a.F, U = a.U;
   const int f0 = strip * P::FO;
   const int f_start = f0 - kHalo;
   char* X = smem;
-  char* Y = smem + R0 * kTP * kHID * (int)sizeof(S);
-  const size_t bu = (size_t)b * U + u;
-  // z chunks: [0,QS) <- a, [QS,2QS) <- s, 2QS <- pe (2 values), rest 0
-  for (int idx = threadIdx.x; idx < R0 * kTP * NQ; idx += 512) {
-    const int q = idx % NQ;
-    const int tt = (idx / NQ) % kTP;
-    const int lf = idx / (NQ * kTP);
-    const int f = f_start + lf;
-    floatx4 zero4 = {0.f, 0.f, 0.f, 0.f};
-    char* dst = X + lds_off<NQ>(lf, tt, q);
-    if (f >= 0 && f < F && tt < kT) {
-      const size_t row = ((bu * F + f) * kTP + tt) * kDSP;
-      if (q < QS) {
-        *reinterpret_cast<floatx4*>(dst) = *reinterpret_cast<const floatx4*>(a.a + row + q * P::EPC);
-      } else if (q < 2 * QS) {
-        *reinterpret_cast<floatx4*>(dst) = *reinterpret_cast<const floatx4*>(a.s_in + row + (q - QS) * P::EPC);
-      } else {
-        *reinterpret_cast<floatx4*>(dst) = zero4;
-        if (q == 2 * QS) {
+  char* WB = smem + R0 * slot_pitch<P>();
+  // z chunks: [0,QS) <- a, [QS,2QS) <- s, 2QS <- pe (2 values), rest 0.  All global
+  // loads of a thread are issued first, then the LDS stores.
+  constexpr int NZ = R0 * kTP * NQ;
+  constexpr int PER = (NZ + 511) / 512;
+  intx4 v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int idx = threadIdx.x + i * 512;
+    v[i] = intx4{0, 0, 0, 0};
+    if (idx < NZ) {
+      const int q = idx % NQ;
+      const int tt = (idx / NQ) % kTP;
+      const int lf = idx / (NQ * kTP);
+      const int f = f_start + lf;
+      if (!(NRX_ABLATE & 2) && f >= 0 && f < F && tt < kT) {
+        const size_t row = srow(b, u, f, tt, U, F);
+        if (q < QS) {
+          v[i] = *reinterpret_cast<const intx4*>(a.a + row + q * P::EPC);
+        } else if (q < 2 * QS) {
+          v[i] = *reinterpret_cast<const intx4*>(a.s_in + row + (q - QS) * P::EPC);
+        } else if (q == 2 * QS) {
           const float* pp = a.pe + (((size_t)u * F + f) * kT + tt) * 2;
-          S* d = reinterpret_cast<S*>(dst);
-          d[0] = (S)pp[0];
-          d[1] = (S)pp[1];
+          S pe2[P::EPC] = {};
+          pe2[0] = (S)pp[0];
+          pe2[1] = (S)pp[1];
+          v[i] = *reinterpret_cast<const intx4*>(pe2);
         }
       }
-    } else {
-      *reinterpret_cast<floatx4*>(dst) = zero4;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int idx = threadIdx.x + i * 512;
+    if (idx < NZ) {
+      const int q = idx % NQ;
+      const int tt = (idx / NQ) % kTP;
+      const int lf = idx / (NQ * kTP);
+      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(lf, tt, q)) = v[i];
     }
   }
   __syncthreads();
-  strip_conv12<P, CINP>(X, Y, f_start, F, prm.w);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int t = lane & 15, g = lane >> 4;
-  typename P::Acc acc[kDSP / 16];
-  for (int lf = kHalo + wave; lf < R0 - kHalo; lf += 8) {
-    const int f = f_start + lf;
-    if (f >= F) continue;
-    sep_tile<P, kHID, kDSP>(X, lf, t, g, lane, prm.w[2], acc);
-    const size_t row = ((bu * F + f) * kTP + t) * kDSP;
-    const S* skip = a.s_in + row;
-    S* dst = a.s_out + row;
-#pragma unroll
-    for (int n = 0; n < kDSP / 16; ++n) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int co = 16 * n + P::co(g, j);
-        Real v = (Real)acc[n][j] + (Real)prm.w[2].b[co] + (Real)skip[co];
-        if (t >= kT || co >= kDS) v = 0;
-        dst[co] = (S)v;
-      }
-    }
-  }
+  stamp(1);
+  strip_conv12<P, kUPD_CINP>(X, WB, f_start, F, prm.w);
+  stamp(3);
+  strip_conv3<P, CHP, TAILM>(prm, X, WB, b, u, f_start, 0, 0, false);
+  stamp(4);
 }
 
-// ========================================================================= k_agg
-// Per RE, all users: sp_u = W2 relu(W1 s_u + b1) + b2, masked by active; a_u = (sum -
-// sp_u) * p, p = 1/max(#active-1) (1 when <= 1 active).  grid = (ceil(F/4), B), block 256:
-// one wave per subcarrier row (16 symbols).
+// ------------------------------------------------------------------------ agg tail
+// Leave-one-out mean over users (neural_rx.py:191-204): a_u = (sum_u' sp_u' - sp_u) * p,
+// sp_u already scaled by act_u, p = 1/max(#active - 1) (1 when <= 1 active).  Run by the
+// last workgroup of the (slot, strip) to arrive; streams a_out in place.
 template <class P>
-struct AggParams {
-  FwdArgs<typename P::WT, typename P::BT, typename P::S> a;
-  DenseW<typename P::WT, typename P::BT> w[2];
-};
-
-template <class P>
-__device__ __forceinline__ void agg_mlp(const typename P::S* srow, char* hid, int t, int g, int lane,
-                                        const DenseW<typename P::WT, typename P::BT>* w,
-                                        typename P::Acc (&out)[kDSP / 16]) {
-  constexpr int NQ_H = kAGG * (int)sizeof(typename P::S) / 16;
-  typename P::Acc h[kAGG / 16];
-  dense_tile<P, kDSP, kAGG>([&](int q) { return P::ld_glb(srow + q * P::EPC); }, lane, g, w[0], h);
-  wave_lds_sync();
-  epi_lds<P, kAGG>(hid, 0, t, g, h, w[0].b, true, false);
-  wave_lds_sync();
-  dense_tile<P, kAGG, kDSP>([&](int q) { return P::ld_lds(hid + lds_off<NQ_H>(0, t, q)); }, lane, g,
-                            w[1], out);
-}
-
-template <class P>
-__global__ __launch_bounds__(256) void k_agg(AggParams<P> prm) {
+__device__ __forceinline__ void tail_combine(const BlockParams<P>& prm, int b, int strip) {
   using S = typename P::S;
   using Real = typename P::Real;
-  __shared__ __attribute__((aligned(16))) char smem[4][kTP * kAGG * sizeof(S)];
   const auto& a = prm.a;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int t = lane & 15, g = lane >> 4;
-  const int f = blockIdx.x * 4 + wave;
-  const int b = blockIdx.y;
   const int F = a.F, U = a.U;
-  if (f >= F) return;
-  char* hid = smem[wave];
   Real nact = 0;
   for (int u = 0; u < U; ++u) nact += (Real)a.active[(size_t)b * U + u];
   Real p = nact - (Real)1;
   p = p > (Real)0 ? p : (Real)0;
   p = p == (Real)0 ? (Real)1 : (Real)1 / p;
-  typename P::Acc sum[kDSP / 16], sp[kDSP / 16];
+  constexpr int QS = kDS / P::EPC;
+  const int f0 = strip * P::FO;
+  const int f1 = f0 + P::FO < F ? f0 + P::FO : F;
+  const int nitem = (f1 - f0) * kT * QS;
+  constexpr int IB = 2;
+  for (int base = threadIdx.x; base < nitem; base += 512 * IB) {
+    intx4 v[IB][kMaxUsers];
 #pragma unroll
-  for (int n = 0; n < kDSP / 16; ++n) sum[n] = P::zero();
-  for (int u = 0; u < U; ++u) {
-    const Real act = (Real)a.active[(size_t)b * U + u];
-    const S* srow = a.s_in + ((((size_t)b * U + u) * F + f) * kTP + t) * kDSP;
-    agg_mlp<P>(srow, hid, t, g, lane, prm.w, sp);
+    for (int i = 0; i < IB; ++i) {
+      const int idx = base + i * 512;
 #pragma unroll
-    for (int n = 0; n < kDSP / 16; ++n)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        sum[n][j] += ((Real)sp[n][j] + (Real)prm.w[1].b[16 * n + P::co(g, j)]) * act;
-  }
-  for (int u = 0; u < U; ++u) {
-    const Real act = (Real)a.active[(size_t)b * U + u];
-    const size_t row = ((((size_t)b * U + u) * F + f) * kTP + t) * kDSP;
-    agg_mlp<P>(a.s_in + row, hid, t, g, lane, prm.w, sp);
-    S* dst = a.a + row;
-#pragma unroll
-    for (int n = 0; n < kDSP / 16; ++n) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int co = 16 * n + P::co(g, j);
-        const Real own = ((Real)sp[n][j] + (Real)prm.w[1].b[co]) * act;
-        Real v = ((Real)sum[n][j] - own) * p;
-        if (t >= kT || co >= kDS) v = 0;
-        dst[co] = (S)v;
-      }
+      for (int uu = 0; uu < kMaxUsers; ++uu)
+        if (uu < U && idx < nitem) {
+          const int q = idx % QS, rowi = idx / QS;
+          v[i][uu] = *reinterpret_cast<const intx4*>(a.a_out + srow(b, uu, f0, 0, U, F) + (size_t)rowi * kDS + q * P::EPC);
+        }
     }
-  }
-}
-
-// ===================================================================== k_readout
-// Per (b, u, subcarrier row): LLR head(s) 56->128->bits and ChEst 56->128->2A.
-template <class P>
-struct ReadParams {
-  FwdArgs<typename P::WT, typename P::BT, typename P::S> a;
-  DenseW<typename P::WT, typename P::BT> llr[kMaxHeads][2];
-  DenseW<typename P::WT, typename P::BT> chest[2];
-};
-
-template <class P, int COUTP>
-__device__ __forceinline__ void head(const typename P::S* srow, char* hid, int t, int g, int lane,
-                                     const DenseW<typename P::WT, typename P::BT>* w,
-                                     typename P::Acc (&out)[COUTP / 16]) {
-  constexpr int NQ_H = kHID * (int)sizeof(typename P::S) / 16;
-  typename P::Acc h[kHID / 16];
-  dense_tile<P, kDSP, kHID>([&](int q) { return P::ld_glb(srow + q * P::EPC); }, lane, g, w[0], h);
-  wave_lds_sync();
-  epi_lds<P, kHID>(hid, 0, t, g, h, w[0].b, true, false);
-  wave_lds_sync();
-  dense_tile<P, kHID, COUTP>([&](int q) { return P::ld_lds(hid + lds_off<NQ_H>(0, t, q)); }, lane, g,
-                             w[1], out);
-}
-
-template <class P, int CHP>
-__global__ __launch_bounds__(256) void k_readout(ReadParams<P> prm) {
-  using S = typename P::S;
-  using Real = typename P::Real;
-  __shared__ __attribute__((aligned(16))) char smem[4][kTP * kHID * sizeof(S)];
-  const auto& a = prm.a;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int t = lane & 15, g = lane >> 4;
-  const int f = blockIdx.x * 4 + wave;
-  const int u = blockIdx.y, b = blockIdx.z;
-  const int F = a.F, U = a.U, B = a.B;
-  if (f >= F) return;
-  char* hid = smem[wave];
-  const size_t bu = (size_t)b * U + u;
-  const S* srow = a.s_in + ((bu * F + f) * kTP + t) * kDSP;
-  for (int hh = 0; hh < a.H; ++hh) {
-    typename P::Acc o[1];
-    head<P, 16>(srow, hid, t, g, lane, prm.llr[hh], o);
-    if (t < kT) {
-      float* dst = a.llr + ((((size_t)hh * B + b) * U + u) * F + f) * kT * a.bits_max + t * a.bits_max;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int co = P::co(g, j);
-        if (co < a.bits_max)
-          dst[co] = co < a.head_bits[hh] ? (float)((Real)o[0][j] + (Real)prm.llr[hh][1].b[co]) : 0.f;
-      }
-    }
-    wave_lds_sync();
-  }
-  if (a.h_ref) {
-    typename P::Acc o[CHP / 16];
-    head<P, CHP>(srow, hid, t, g, lane, prm.chest, o);
-    if (t < kT) {
-      const int A2 = 2 * a.A;
-      float* dst = a.h_ref + ((bu * F + f) * kT + t) * A2;
+    for (int i = 0; i < IB; ++i) {
+      const int idx = base + i * 512;
+      if (idx >= nitem) continue;
+      const int q = idx % QS, rowi = idx / QS;
+      Real sum[P::EPC];
 #pragma unroll
-      for (int n = 0; n < CHP / 16; ++n)
+      for (int e = 0; e < P::EPC; ++e) sum[e] = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int co = 16 * n + P::co(g, j);
-          if (co < A2) dst[co] = (float)((Real)o[n][j] + (Real)prm.chest[1].b[co]);
+      for (int uu = 0; uu < kMaxUsers; ++uu)
+        if (uu < U) {
+          const S* sv = reinterpret_cast<const S*>(&v[i][uu]);
+#pragma unroll
+          for (int e = 0; e < P::EPC; ++e) sum[e] += (Real)sv[e];
+        }
+#pragma unroll
+      for (int uu = 0; uu < kMaxUsers; ++uu)
+        if (uu < U) {
+          const S* sv = reinterpret_cast<const S*>(&v[i][uu]);
+          S o[P::EPC];
+#pragma unroll
+          for (int e = 0; e < P::EPC; ++e) o[e] = (S)((sum[e] - (Real)sv[e]) * p);
+          *reinterpret_cast<intx4*>(a.a_out + srow(b, uu, f0, 0, U, F) + (size_t)rowi * kDS + q * P::EPC) =
+              *reinterpret_cast<const intx4*>(o);
         }
     }
   }
+}
+
+// Arrival ticket after this workgroup's stores (cdna_hip_programming.md section 6
+// Guideline 16, counter form): every workgroup publishes its rows with an agent-scope
+// release; the one drawing the last ticket acquires and combines.  Correct for any
+// placement of the user workgroups over CUs/XCDs.
+template <class P, int TAILM>
+__device__ __forceinline__ void run_tail(const BlockParams<P>& prm, char* smem, int b, int strip, int strips) {
+  if (TAILM != TAIL_AGG || (NRX_ABLATE & 8)) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // every wave's stores done
+  __syncthreads();
+  unsigned* flag = reinterpret_cast<unsigned*>(smem);
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(prm.counters + (size_t)b * strips + strip, 1u,
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned last = old == (unsigned)(prm.a.U - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  const bool last = *flag != 0;
+  if (last) tail_combine<P>(prm, b, strip);
+}
+
+// StateInit_m (+ Var-IO mix: one launch per m, m > 0 accumulating) of one (slot, user,
+// strip); the last launch applies the aggregation MLP of iteration 0.  grid = (strips, U, B).
+template <class P, int CINP, int CHP, int TAILM>
+__global__ __launch_bounds__(512) void k_init(BlockParams<P> prm) {
+  using Real = typename P::Real;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const auto& a = prm.a;
+  const int strip = blockIdx.x, u = blockIdx.y, b = blockIdx.z;
+  const int U = a.U;
+  const int m = prm.m;
+  Real wm = (Real)1;
+  if (!a.masking)
+    wm = a.mcs_mask ? (Real)a.mcs_mask[((size_t)b * U + u) * a.M + m] : (Real)(m == 0 ? 1 : 0);
+  // wm == 0: this MCS contributes exactly 0 * finite; the conv math is still run (the
+  // m = 0 launch defines s, the last launch applies the aggregation MLP).
+  init_user<P, CINP, CHP, TAILM>(prm, smem, b, u, strip, wm, m == 0);
+  run_tail<P, TAILM>(prm, smem, b, strip, gridDim.x);
+}
+
+// UpdateState of one (slot, user, strip), then the tail.  grid = (strips, U, B).
+template <class P, int CHP, int TAILM>
+__global__ __launch_bounds__(512) void k_update(BlockParams<P> prm) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int strip = blockIdx.x, u = blockIdx.y, b = blockIdx.z;
+  stamp(0);
+  update_user<P, CHP, TAILM>(prm, smem, b, u, strip);
+  run_tail<P, TAILM>(prm, smem, b, strip, gridDim.x);
+  stamp(5);
 }
 
 // ======================================================================= launchers
@@ -605,76 +1042,91 @@ struct Launch {
 
   static hipError_t setup() {
     hipError_t e = hipSuccess;
-    auto set = [&](const void* f, int bytes) {
-      hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    auto set = [&](const void* f) {
+      hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, strip_lds_bytes<P>());
       if (r != hipSuccess) e = r;
     };
-    set((const void*)k_init<P, 32>, strip_lds_bytes<P>(32));
-    set((const void*)k_init<P, 64>, strip_lds_bytes<P>(64));
-    set((const void*)k_init<P, 128>, strip_lds_bytes<P>(128));
-    set((const void*)k_update<P>, strip_lds_bytes<P>(kUPD_CINP));
+#define NRX_SET_INIT(C, CH)                                   \
+    set((const void*)k_init<P, C, CH, TAIL_NONE>);            \
+    set((const void*)k_init<P, C, CH, TAIL_AGG>);
+    NRX_SET_INIT(32, 16) NRX_SET_INIT(64, 16) NRX_SET_INIT(128, 16)
+    NRX_SET_INIT(32, 32) NRX_SET_INIT(64, 32) NRX_SET_INIT(128, 32)
+#undef NRX_SET_INIT
+    set((const void*)k_update<P, 16, TAIL_AGG>);
+    set((const void*)k_update<P, 16, TAIL_READOUT>);
+    set((const void*)k_update<P, 32, TAIL_AGG>);
+    set((const void*)k_update<P, 32, TAIL_READOUT>);
     return e;
+  }
+
+  template <int C, int CH>
+  static void launch_init(dim3 grid, int L, hipStream_t st, const BlockParams<P>& bp, bool tail) {
+    if (tail) k_init<P, C, CH, TAIL_AGG><<<grid, 512, L, st>>>(bp);
+    else k_init<P, C, CH, TAIL_NONE><<<grid, 512, L, st>>>(bp);
   }
 
   static hipError_t run(const A& args0, const MW& W, int num_it, hipStream_t st, Prof* prof) {
     A args = args0;
     const int strips = (args.F + P::FO - 1) / P::FO;
+    constexpr int L = strip_lds_bytes<P>();
+    const bool ch32 = 2 * args.A > 16;
     auto B_ = [&](int k) { if (prof) prof->begin(k, st); };
     auto E_ = [&](int k) { if (prof) prof->end(k, st); };
+    BlockParams<P> bp;
+    bp.a = args;
+    {
+      // arrival tickets of the aggregation tails: zeroed on the stream every forward
+      const size_t bytes = (size_t)(num_it + 1) * args.B * strips * sizeof(unsigned);
+      hipError_t e = hipMemsetAsync(args.counters, 0, bytes, st);
+      if (e != hipSuccess) return e;
+    }
+    for (int h = 0; h < args.H; ++h) {
+      bp.llr[h][0] = W.llr[h][0];
+      bp.llr[h][1] = W.llr[h][1];
+    }
+    bp.chest[0] = W.chest[0];
+    bp.chest[1] = W.chest[1];
     B_(K_NORM);
     k_norm<<<args.B, 256, 0, st>>>(args.y, args.F * kT * 2 * args.A, args.norm);
     E_(K_NORM);
+    // StateInit -> s_out; tail of the last StateInit launch: aggregation of iteration 0
+    const size_t ncnt = (size_t)args.B * strips;
+    dim3 grid(strips, args.U, args.B);
     B_(K_INIT);
-    {
-      InitParams<P> ip;
-      ip.a = args;
-      for (int m = 0; m < args.num_init; ++m)
-        for (int l = 0; l < 3; ++l) ip.w[m][l] = W.init[m][l];
-      dim3 grid(strips, args.U, args.B);
-      if (args.init_cinp <= 32) {
-        constexpr int L = strip_lds_bytes<P>(32);
-        k_init<P, 32><<<grid, 512, L, st>>>(ip);
-      } else if (args.init_cinp <= 64) {
-        constexpr int L = strip_lds_bytes<P>(64);
-        k_init<P, 64><<<grid, 512, L, st>>>(ip);
-      } else {
-        constexpr int L = strip_lds_bytes<P>(128);
-        k_init<P, 128><<<grid, 512, L, st>>>(ip);
-      }
+    for (int m = 0; m < args.num_init; ++m) {
+      for (int l = 0; l < 3; ++l) bp.w[l] = W.init[m][l];
+      bp.m = m;
+      bp.tail = m == args.num_init - 1 ? TAIL_AGG : TAIL_NONE;
+      bp.counters = args.counters;
+      bp.agg[0] = W.agg[0][0];
+      bp.agg[1] = W.agg[0][1];
+      const bool tl = bp.tail == TAIL_AGG;
+      if (args.init_cinp <= 32) ch32 ? launch_init<32, 32>(grid, L, st, bp, tl) : launch_init<32, 16>(grid, L, st, bp, tl);
+      else if (args.init_cinp <= 64) ch32 ? launch_init<64, 32>(grid, L, st, bp, tl) : launch_init<64, 16>(grid, L, st, bp, tl);
+      else ch32 ? launch_init<128, 32>(grid, L, st, bp, tl) : launch_init<128, 16>(grid, L, st, bp, tl);
     }
     E_(K_INIT);
-    constexpr int LU = strip_lds_bytes<P>(kUPD_CINP);
     for (int i = 0; i < num_it; ++i) {
-      // s_out of the previous stage is this iteration's input
-      std::swap(args.s_in, args.s_out);
-      AggParams<P> ap;
-      ap.a = args;
-      ap.w[0] = W.agg[i][0];
-      ap.w[1] = W.agg[i][1];
-      B_(K_AGG);
-      k_agg<P><<<dim3((args.F + 3) / 4, args.B), 256, 0, st>>>(ap);
-      E_(K_AGG);
-      UpdParams<P> up;
-      up.a = args;
-      for (int l = 0; l < 3; ++l) up.w[l] = W.upd[i][l];
+      std::swap(bp.a.s_in, bp.a.s_out);
+      std::swap(bp.a.a, bp.a.a_out);
+      for (int l = 0; l < 3; ++l) bp.w[l] = W.upd[i][l];
+      const bool last = i == num_it - 1;
+      bp.tail = last ? TAIL_READOUT : TAIL_AGG;
+      bp.counters = args.counters + (size_t)(i + 1) * ncnt;
+      if (!last) {
+        bp.agg[0] = W.agg[i + 1][0];
+        bp.agg[1] = W.agg[i + 1][1];
+      }
       B_(K_UPDATE);
-      k_update<P><<<dim3(strips, args.U, args.B), 512, LU, st>>>(up);
+      if (last) {
+        if (ch32) k_update<P, 32, TAIL_READOUT><<<grid, 512, L, st>>>(bp);
+        else k_update<P, 16, TAIL_READOUT><<<grid, 512, L, st>>>(bp);
+      } else {
+        if (ch32) k_update<P, 32, TAIL_AGG><<<grid, 512, L, st>>>(bp);
+        else k_update<P, 16, TAIL_AGG><<<grid, 512, L, st>>>(bp);
+      }
       E_(K_UPDATE);
     }
-    std::swap(args.s_in, args.s_out);
-    ReadParams<P> rp;
-    rp.a = args;
-    for (int h = 0; h < args.H; ++h) {
-      rp.llr[h][0] = W.llr[h][0];
-      rp.llr[h][1] = W.llr[h][1];
-    }
-    rp.chest[0] = W.chest[0];
-    rp.chest[1] = W.chest[1];
-    dim3 grid((args.F + 3) / 4, args.U, args.B);
-    B_(K_READOUT);
-    if (2 * args.A <= 16) k_readout<P, 16><<<grid, 256, 0, st>>>(rp);
-    else k_readout<P, 32><<<grid, 256, 0, st>>>(rp);
-    E_(K_READOUT);
     return hipGetLastError();
   }
 };
@@ -698,5 +1150,11 @@ hipError_t setup_kernels() {
 }
 
 int strip_width(int precision) { return precision == 0 ? P16::FO : P64::FO; }
+
+#ifdef NRX_STAMPS
+extern "C" int nrx_debug_stamps(void* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nrx_stamps), (size_t)n * 8 * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 }  // namespace nrx

@@ -26,6 +26,17 @@ def kernel_flops_per_re_user(spec: ModelSpec) -> dict:
     return {"norm": 0, "state_init": init, "aggregate": agg, "state_update": upd, "readout": ro}
 
 
+def launch_flops_per_re_user(spec: ModelSpec, num_it: int) -> dict:
+    """Algorithmic FLOPs per RE-user of each *launch* of the engine's kernels, as fused:
+    k_init = StateInit(s) + aggregation MLP of iteration 0 (tail); k_update (average
+    over its num_it launches) = state update + the next aggregation MLP, or the readouts
+    after the last iteration."""
+    k = kernel_flops_per_re_user(spec)
+    return {"norm": 0,
+            "state_init": k["state_init"] + k["aggregate"],
+            "state_update": k["state_update"] + ((num_it - 1) * k["aggregate"] + k["readout"]) / num_it}
+
+
 def forward_flops_per_re_user(spec: ModelSpec, num_it: int) -> int:
     k = kernel_flops_per_re_user(spec)
     return k["state_init"] + num_it * (k["aggregate"] + k["state_update"]) + k["readout"]

@@ -1,0 +1,33 @@
+"""Diagnostic: per-phase cycle shares of k_update (NRX_STAMPS build)."""
+import ctypes, os, sys, subprocess
+import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                "-DNRX_STAMPS", "neural_rx_amd/csrc/nrx_kernels.hip", "neural_rx_amd/csrc/nrx_api.cpp",
+                "-o", "/tmp/libnrx_stamps.so"], check=True)
+import torch
+from neural_rx_amd import _lib
+lib = _lib.load("/tmp/libnrx_stamps.so")
+lib.nrx_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+from neural_rx_amd import synth, weights as W
+from neural_rx_amd.config import get_config, spec_from_config, dmrs_symbols, user_cdm_groups
+from neural_rx_amd.receiver import CGNNEngine, compute_pe
+cfg = get_config("nrx_rt"); spec = spec_from_config(cfg)
+B, U, prbs = 128, 2, 4
+sl = synth.generate(B, U, prbs, 4, [4, 4], (0, 1), snr_db=10, seed=3)
+eng = CGNNEngine(spec, W.load("nrx_rt"))
+t = lambda a: torch.from_numpy(a).cuda()
+pe = t(compute_pe(U, 48, (2, 11), (0, 1)))
+for _ in range(5):
+    eng.forward(t(sl.y), pe, t(sl.h_hat), t(sl.active), None, 2, "f16")
+torch.cuda.synchronize()
+n = 512
+buf = np.zeros((n, 8), np.uint64)
+lib.nrx_debug_stamps(buf.ctypes.data, n)
+st = buf[:, :6].astype(np.int64)
+d = np.diff(st, axis=1)
+names = ["z-load", "conv1", "conv2", "conv3+epi", "tail"]
+tot = st[:, 5] - st[:, 0]
+print("cycles per WG (mean):", tot.mean(), " start spread:", st[:, 0].max() - st[:, 0].min())
+for i, nm in enumerate(names):
+    print(f"  {nm:10s} mean {d[:, i].mean():9.0f}  ({100 * d[:, i].mean() / tot.mean():5.1f}%)  max {d[:, i].max()}")
