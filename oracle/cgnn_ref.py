@@ -204,39 +204,6 @@ def load_npz_weights(path: str) -> List[np.ndarray]:
     return [d[f"w{i:03d}"] for i in range(int(d["count"]))]
 
 
-def seeded_weights(spec, seed: int = 0) -> List[np.ndarray]:
-    """Random Keras-ordered weights for topologies with no trained weights (BASELINE
-    config 3: nrx_large topology with 16 rx antennas).  Glorot-uniform kernels,
-    small biases, like a freshly initialised Keras model."""
-    rng = np.random.default_rng(seed)
-    out: List[np.ndarray] = []
-
-    def glorot(shape, fan_in, fan_out):
-        lim = np.sqrt(6.0 / (fan_in + fan_out))
-        return rng.uniform(-lim, lim, size=shape).astype(np.float32)
-
-    def sep(cin, cout):
-        out.append(glorot((3, 3, cin, 1), 9, 9))
-        out.append(glorot((1, 1, cin, cout), cin, cout))
-        out.append(rng.uniform(-0.05, 0.05, size=(cout,)).astype(np.float32))
-
-    def dense_(cin, cout):
-        out.append(glorot((cin, cout), cin, cout))
-        out.append(rng.uniform(-0.05, 0.05, size=(cout,)).astype(np.float32))
-
-    u1, u2 = spec.init_units
-    for _ in range(spec.num_init):
-        sep(spec.init_in_ch, u1); sep(u1, u2); sep(u2, spec.d_s)
-    v1, v2 = spec.state_units
-    for _ in range(spec.num_it):
-        dense_(spec.d_s, spec.agg_units); dense_(spec.agg_units, spec.d_s)
-        sep(spec.update_in_ch, v1); sep(v1, v2); sep(v2, spec.d_s)
-    for nb in spec.head_bits:
-        dense_(spec.d_s, spec.readout_units); dense_(spec.readout_units, nb)
-    dense_(spec.d_s, spec.readout_units); dense_(spec.readout_units, 2 * spec.num_rx_ant)
-    return out
-
-
 def count_params(spec) -> Dict[str, int]:
     """Per-block parameter counts (cf. nrx_architecture.ipynb:295-308)."""
     def sep(ci, co):

@@ -1,0 +1,115 @@
+"""Generate golden vectors from the reference's own torch sub-modules.
+
+Runs in the build container only (needs /root/reference).  The reference file
+``utils/neural_rx.py`` imports Sionna and TensorFlow at module level (lines 22-30);
+neither is installed, so empty placeholder modules are registered for those names
+before importing it.  Only sub-modules whose torch port is semantically correct are
+exercised:
+
+* ``AggregateUserStates`` (neural_rx.py:135-207) with the RE axes folded into the
+  batch axis (the port broadcasts ``active_tx`` against a rank-3 state only),
+* ``ReadoutLLRs`` (neural_rx.py:309-355) and ``ReadoutChEst`` (neural_rx.py:358-404),
+* ``NRPreprocessing._focc_removal`` (neural_rx.py:1620-1629).
+
+The trained nrx_rt weights (Keras Dense kernels ``[in, out]``) are loaded into the
+``nn.Linear`` layers transposed.  Output: ``tests/golden/ref_modules_nrx_rt.npz``
+(inputs and outputs only -- data, no reference code).
+
+    python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import importlib.util
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+REF = "/root/reference/utils/neural_rx.py"
+
+
+def _placeholder_modules():
+    """Register empty modules for the Sionna / TensorFlow names the file imports."""
+    sionna = types.ModuleType("sionna")
+    utils = types.ModuleType("sionna.utils")
+    utils.flatten_last_dims = lambda *a, **k: None
+    ofdm = types.ModuleType("sionna.ofdm")
+    ofdm.ResourceGridDemapper = object
+    nr = types.ModuleType("sionna.nr")
+    nr.TBDecoder = object
+    nr.LayerDemapper = object
+    sionna.utils, sionna.ofdm, sionna.nr = utils, ofdm, nr
+    tf = types.ModuleType("tensorflow")
+    for name, mod in [("sionna", sionna), ("sionna.utils", utils), ("sionna.ofdm", ofdm),
+                      ("sionna.nr", nr), ("tensorflow", tf)]:
+        sys.modules.setdefault(name, mod)
+
+
+def main():
+    import torch
+    from neural_rx_amd import weights as W
+
+    _placeholder_modules()
+    spec = importlib.util.spec_from_file_location("ref_neural_rx", REF)
+    ref = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ref)
+
+    w = W.load("nrx_rt")
+    rng = np.random.default_rng(20241016)
+    out = {}
+
+    def set_linear(lin, kernel, bias):
+        with torch.no_grad():
+            lin.weight.copy_(torch.from_numpy(kernel.T.copy()))
+            lin.bias.copy_(torch.from_numpy(bias))
+
+    # AggregateUserStates of iteration 0 (weights 9-12): RE axes folded into the batch
+    agg = ref.AggregateUserStates(56, [64], 56)
+    set_linear(agg._hidden_layers[0], w[9], w[10])
+    set_linear(agg._output_layer, w[11], w[12])
+    n, u = 64, 2
+    s = (rng.standard_normal((n, u, 56)) * 3).astype(np.float32)
+    act = np.ones((n, u), np.float32)
+    act[:8, 1] = 0.0          # single active user rows
+    act[8:12, :] = 0.0        # no active user rows
+    with torch.no_grad():
+        a = agg((torch.from_numpy(s), torch.from_numpy(act))).numpy()
+    out.update(agg_s=s, agg_active=act, agg_a=a)
+    # four users
+    s4 = (rng.standard_normal((32, 4, 56)) * 3).astype(np.float32)
+    act4 = (rng.random((32, 4)) > 0.3).astype(np.float32)
+    with torch.no_grad():
+        a4 = agg((torch.from_numpy(s4), torch.from_numpy(act4))).numpy()
+    out.update(agg4_s=s4, agg4_active=act4, agg4_a=a4)
+
+    # ReadoutLLRs (35-38) and ReadoutChEst (39-42)
+    llr_head = ref.ReadoutLLRs(4, [128], 56)
+    set_linear(llr_head._hidden_layers[0], w[35], w[36])
+    set_linear(llr_head._output_layer, w[37], w[38])
+    ch_head = ref.ReadoutChEst(4, [128], 56)
+    set_linear(ch_head._hidden_layers[0], w[39], w[40])
+    set_linear(ch_head._output_layer, w[41], w[42])
+    sr = (rng.standard_normal((256, 56)) * 5).astype(np.float32)
+    with torch.no_grad():
+        out["ro_s"] = sr
+        out["ro_llr"] = llr_head(torch.from_numpy(sr)).numpy()
+        out["ro_h"] = ch_head(torch.from_numpy(sr)).numpy()
+
+    # NRPreprocessing._focc_removal
+    pre = ref.NRPreprocessing(2)
+    hls = rng.standard_normal((2, 4, 2, 48)).astype(np.float32)
+    with torch.no_grad():
+        out["focc_in"] = hls
+        out["focc_out"] = pre._focc_removal(torch.from_numpy(hls)).numpy()
+
+    path = os.path.join(HERE, "ref_modules_nrx_rt.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", os.path.relpath(path, ROOT), {k: v.shape for k, v in out.items()})
+
+
+if __name__ == "__main__":
+    main()

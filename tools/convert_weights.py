@@ -39,9 +39,11 @@ LABELS = [
 
 _ALLOWED_GLOBALS = {
     ("numpy.core.multiarray", "_reconstruct"),
+    ("numpy._core.multiarray", "_reconstruct"),   # numpy >= 2 spelling
     ("numpy", "ndarray"),
     ("numpy", "dtype"),
 }
+_RECONSTRUCT = {("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct")}
 
 
 class _Global:
@@ -111,7 +113,7 @@ def read_weight_list(path: str) -> list[np.ndarray]:
             fn = stack.pop()
             if not isinstance(fn, _Global):
                 raise ValueError("REDUCE on a non-global")
-            if fn.key == ("numpy.core.multiarray", "_reconstruct"):
+            if fn.key in _RECONSTRUCT:
                 stack.append(_ArrayStub())
             elif fn.key == ("numpy", "dtype"):
                 stack.append(_DtypeStub(args[0]))
