@@ -150,6 +150,8 @@ def main():
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "kernel": "k_update (3 sep-convs + fused aggregation/readout tail)",
                 "flops_per_launch": dom_flops,
+                "algorithmic_bytes_per_launch": round(metrics.update_launch_bytes_per_re_user(
+                    spec, num_it, 2 if args.precision == "f16" else 4) * re_users),
                 "avg_launch_us": round(dom_avg_s * 1e6, 3)}
     whole_tflops = metrics.forward_flops_per_re_user(spec, num_it) * re_users * world / (elapsed / args.steps) / 1e12
 

@@ -4,13 +4,16 @@
 // the TF structure of "neural_rx copy_pytorch.py" (StateInit :82-188, AggregateUserStates
 // :191-231, UpdateState :234-287, ReadoutLLRs/ChEst :324-362).
 //
-// Kernel map (one launch each, per forward):
-//   k_norm      per-slot 1/sqrt(mean(y^2))                       (neural_rx.py:551-557)
+// Kernel map (per forward: 1 + M_init + num_it launches):
+//   k_norm      per-slot 1/sqrt(mean(y^2)), divide-no-nan        (neural_rx.py:551-557)
 //   k_init      StateInit: z=[y,pe,h] -> 3 separable convs       (copy_pytorch.py:160-188)
-//               fused with the Var-IO mcs mix                    (neural_rx.py:562-569)
-//   k_agg       per-RE user aggregation MLP + leave-one-out mean (neural_rx.py:135-207)
+//               one launch per init head m, accumulating the Var-IO mcs mix
+//               (neural_rx.py:562-569); the last one runs the aggregation MLP of
+//               iteration 0 in its conv3 epilogue and the leave-one-out user combine
+//               in a last-arriver tail                            (neural_rx.py:135-207)
 //   k_update    z=[a,s,pe] -> 3 separable convs + skip           (copy_pytorch.py:267-287)
-//   k_readout   LLR head(s) + ChEst head                          (neural_rx.py:309-404)
+//               epilogue: next iteration's aggregation MLP + tail, or after the last
+//               iteration the LLR head(s) + ChEst head           (neural_rx.py:309-404)
 //
 // Tiling.  The resource grid of one (slot, user) is an F x 16 image (T = 14 padded to 16
 // with zero rows).  One MFMA tile = one subcarrier row: 16 symbols x 16 output channels.

@@ -37,6 +37,16 @@ def launch_flops_per_re_user(spec: ModelSpec, num_it: int) -> dict:
             "state_update": k["state_update"] + ((num_it - 1) * k["aggregate"] + k["readout"]) / num_it}
 
 
+def update_launch_bytes_per_re_user(spec: ModelSpec, num_it: int, elem: int = 2) -> float:
+    """Algorithmic HBM bytes per RE-user of one k_update launch (average over num_it):
+    non-last launches read s, a and write s', act*sp; the last reads s, a and writes the
+    f32 LLRs of every head and the f32 ChEst (pe is shared over slots and not counted)."""
+    st = spec.d_s * elem
+    mid = 4 * st
+    last = 2 * st + 4 * (spec.bits_max * spec.num_llr_heads + 2 * spec.num_rx_ant)
+    return ((num_it - 1) * mid + last) / num_it
+
+
 def forward_flops_per_re_user(spec: ModelSpec, num_it: int) -> int:
     k = kernel_flops_per_re_user(spec)
     return k["state_init"] + num_it * (k["aggregate"] + k["state_update"]) + k["readout"]
