@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
 #include <utility>
 
 #include "nrx_internal.h"
@@ -96,6 +97,10 @@ struct P16 {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
   }
   __device__ static int co(int g, int j) { return 4 * g + j; }
+  // accumulator-layout bias of output tile n (C operand of the first MFMA of a chain)
+  __device__ static Acc bias_acc(const float* b, int n, int g) {
+    return *reinterpret_cast<const floatx4*>(b + 16 * n + 4 * g);
+  }
   __device__ static DV shr(DV v) {
     intx4 x = __builtin_bit_cast(intx4, v);
     x = intx4{dpp_shr1(x[0]), dpp_shr1(x[1]), dpp_shr1(x[2]), dpp_shr1(x[3])};
@@ -144,6 +149,9 @@ struct P64 {
     return c;
   }
   __device__ static int co(int g, int j) { return g + 4 * j; }
+  __device__ static Acc bias_acc(const double* b, int n, int g) {
+    return Acc{b[16 * n + g], b[16 * n + g + 4], b[16 * n + g + 8], b[16 * n + g + 12]};
+  }
   __device__ static DV shr(DV v) {
     intx8 x = __builtin_bit_cast(intx8, v);
 #pragma unroll
@@ -212,7 +220,9 @@ struct WLds {
   __device__ typename P::DV dwv(int tap, int kc, int g) const {
     return *reinterpret_cast<const half8*>(base + kWPw + (tap * CINP + kc * 32 + g * 8) * 2);
   }
-  __device__ float bias(int co) const { return reinterpret_cast<const float*>(base + kWBias)[co]; }
+  __device__ typename P::Acc bias_acc(int n, int g) const {
+    return P::bias_acc(reinterpret_cast<const float*>(base + kWBias), n, g);
+  }
 };
 
 template <class P, int CINP, int COUTP>
@@ -224,7 +234,7 @@ struct WGlb {
   __device__ typename P::DV dwv(int tap, int kc, int g) const {
     return P::ld_w(w.dw + tap * CINP + kc * P::KC + g * P::CPL);
   }
-  __device__ typename P::BT bias(int co) const { return w.b[co]; }
+  __device__ typename P::Acc bias_acc(int n, int g) const { return P::bias_acc(w.b, n, g); }
 };
 
 // Cooperative copy of one separable layer's packed weights into the LDS image.  All
@@ -264,22 +274,53 @@ __device__ __forceinline__ void stage_weights(char* wb, const SepW<_Float16, flo
 }
 
 // R consecutive output rows (input slots s0 .. s0+R-1, neighbours s0-1 and s0+R) of one
-// wave, all COUTP channels, pre-bias.  acc[r][n][j] = out[row r][co = 16 n + P::co(g,j)][t].
-// The depthwise weights and every pointwise A fragment are loaded once per K chunk and
-// reused over the R rows; the three input rows of consecutive outputs overlap, so a pass
-// reads R + 2 activation rows instead of 3 R.
+// wave, all COUTP channels, bias included (it is the C operand of the first K chunk).
+// acc[r][n][j] = out[row r][co = 16 n + P::co(g,j)][t].  The depthwise weights and every
+// pointwise A fragment are loaded once per K chunk and reused over the R rows; the three
+// input rows of consecutive outputs overlap, so a pass reads R + 2 activation rows
+// instead of 3 R.
+template <class P, int CINP, int COUTP, bool FIRST, class WS>
+__device__ __forceinline__ void conv_chunk(const char* X, const int (&rb)[P::R + 2], int sw, int kc, int g,
+                                           int lane, const WS& ws, typename P::Acc (&acc)[P::R][COUTP / 16]) {
+  using DV = typename P::DV;
+  constexpr int R = P::R;
+  const int off = ((kc * 4 + g) ^ sw) * 16;
+  DV xs[R + 2];
+#pragma unroll
+  for (int i = 0; i < R + 2; ++i) xs[i] = P::ld_lds(X + rb[i] + off);
+  DV w[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) w[k] = ws.dwv(k, kc, g);
+  DV d[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    // column sums per symbol offset dt = j - 1 (tap = i*3 + j, i along subcarriers)
+    const DV cm = w[0] * xs[r] + w[3] * xs[r + 1] + w[6] * xs[r + 2];
+    const DV c0 = w[1] * xs[r] + w[4] * xs[r + 1] + w[7] * xs[r + 2];
+    const DV cp = w[2] * xs[r] + w[5] * xs[r + 1] + w[8] * xs[r + 2];
+    d[r] = c0 + P::shr(cm) + P::shl(cp);
+  }
+#pragma unroll
+  for (int n = 0; n < COUTP / 16; ++n) {
+    const DV a = ws.afrag(n, kc, lane, g);
+    if constexpr (FIRST) {
+      const typename P::Acc bn = ws.bias_acc(n, g);
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r][n] = P::mma_v(a, d[r], bn);
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r][n] = P::mma_v(a, d[r], acc[r][n]);
+    }
+  }
+}
+
 template <class P, int CINP, int COUTP, class WS>
 __device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int t, int g, int lane,
                                           const WS& ws,
                                           typename P::Acc (&acc)[P::R][COUTP / 16]) {
-  using DV = typename P::DV;
   constexpr int R = P::R;
   constexpr int NQ = CINP * (int)sizeof(typename P::S) / 16;
   constexpr int NKC = CINP / P::KC;
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-#pragma unroll
-    for (int n = 0; n < COUTP / 16; ++n) acc[r][n] = P::zero();
   const int sw = swz<NQ>(t);
   int rb[R + 2];
 #pragma unroll
@@ -288,30 +329,8 @@ __device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int
     sl = sl < 0 ? 0 : (sl >= nslots ? nslots - 1 : sl);
     rb[i] = sl * slot_pitch<P>() + t * NQ * 16;
   }
-  for (int kc = 0; kc < NKC; ++kc) {
-    const int off = ((kc * 4 + g) ^ sw) * 16;
-    DV xs[R + 2];
-#pragma unroll
-    for (int i = 0; i < R + 2; ++i) xs[i] = P::ld_lds(X + rb[i] + off);
-    DV w[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) w[k] = ws.dwv(k, kc, g);
-    DV d[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      // column sums per symbol offset dt = j - 1 (tap = i*3 + j, i along subcarriers)
-      const DV cm = w[0] * xs[r] + w[3] * xs[r + 1] + w[6] * xs[r + 2];
-      const DV c0 = w[1] * xs[r] + w[4] * xs[r + 1] + w[7] * xs[r + 2];
-      const DV cp = w[2] * xs[r] + w[5] * xs[r + 1] + w[8] * xs[r + 2];
-      d[r] = c0 + P::shr(cm) + P::shl(cp);
-    }
-#pragma unroll
-    for (int n = 0; n < COUTP / 16; ++n) {
-      const DV a = ws.afrag(n, kc, lane, g);
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r][n] = P::mma_v(a, d[r], acc[r][n]);
-    }
-  }
+  conv_chunk<P, CINP, COUTP, true>(X, rb, sw, 0, g, lane, ws, acc);
+  for (int kc = 1; kc < NKC; ++kc) conv_chunk<P, CINP, COUTP, false>(X, rb, sw, kc, g, lane, ws, acc);
 }
 
 // One layer over output positions [pos_lo, pos_hi) in rounds of 8 waves x R rows.  Every
@@ -327,51 +346,71 @@ __device__ __forceinline__ void conv_layer(const char* X, int nslots, int in_off
     const int p0 = base + wave * P::R;
     const bool act = p0 < pos_hi;
     typename P::Acc acc[P::R][COUTP / 16];
+    typename std::decay_t<Epi>::Pref pf;
+    if (act) epi.prefetch(pf, p0, t, g);     // epilogue global loads, in flight during the math
     if (act) {
       if constexpr (NRX_ABLATE & 1) {
 #pragma unroll
         for (int r = 0; r < P::R; ++r)
 #pragma unroll
-          for (int n = 0; n < COUTP / 16; ++n) acc[r][n] = P::zero();
+          for (int n = 0; n < COUTP / 16; ++n) acc[r][n] = ws.bias_acc(n, g);
       } else {
         conv_rows<P, CINP, COUTP>(X, p0 - in_off, nslots, t, g, lane, ws, acc);
       }
     }
     __syncthreads();
     epi.pre();                       // all threads (e.g. stage tail weights into X)
-    if (act) epi(acc, p0, t, g);
+    if (act) epi(acc, pf, p0, t, g);
     __syncthreads();
   }
 }
 
-// In-place epilogue: +bias, ReLU, zero outside the grid / t >= 14, store to slot p-in_off-1.
+struct NoPref {};
+
+// In-place epilogue: ReLU, zero outside the grid, store to slot p-in_off-1.  Lanes
+// t >= 14 do not store: the pad symbols of every slot are zero from the start of the
+// block and stay zero (P16); P64 writes them as zeros.
 template <class P, int COUTP, class WS>
 struct EpiInPlace {
+  using Pref = NoPref;
   char* X;
   int in_off, pos_hi, f_start, F;
   WS ws;
   __device__ void pre() const {}
-  __device__ void operator()(const typename P::Acc (&acc)[P::R][COUTP / 16], int p0, int t, int g) const {
+  __device__ void prefetch(Pref&, int, int, int) const {}
+  __device__ void operator()(const typename P::Acc (&acc)[P::R][COUTP / 16], const Pref&, int p0, int t,
+                             int g) const {
     using Real = typename P::Real;
-    constexpr int NQ = COUTP * (int)sizeof(typename P::S) / 16;
+    using S = typename P::S;
+    constexpr int NQ = COUTP * (int)sizeof(S) / 16;
 #pragma unroll
     for (int r = 0; r < P::R; ++r) {
       const int p = p0 + r;
       if (p >= pos_hi) continue;
       const int f = f_start + p;
-      const bool z = f < 0 || f >= F || t >= kT;
+      const bool z = f < 0 || f >= F;
       const int slot = p - in_off - 1;
+      if constexpr (sizeof(S) == 2) {
+        if (t < kT) {
 #pragma unroll
-      for (int n = 0; n < COUTP / 16; ++n) {
+          for (int n = 0; n < COUTP / 16; ++n) {
+            half4 h = half4{(S)acc[r][n][0], (S)acc[r][n][1], (S)acc[r][n][2], (S)acc[r][n][3]};
+            h = __builtin_elementwise_max(h, half4{0, 0, 0, 0});
+            if (z) h = half4{0, 0, 0, 0};
+            *reinterpret_cast<half4*>(X + xoff<P, NQ>(slot, t, 2 * n + (g >> 1)) + (g & 1) * 8) = h;
+          }
+        }
+      } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int co = 16 * n + P::co(g, j);
-          Real v = (Real)acc[r][n][j] + (Real)ws.bias(co);
-          v = v > (Real)0 ? v : (Real)0;
-          if (z) v = (Real)0;
-          *reinterpret_cast<typename P::S*>(X + xoff<P, NQ>(slot, t, co / P::EPC) +
-                                            (co % P::EPC) * (int)sizeof(typename P::S)) =
-              (typename P::S)v;
+        for (int n = 0; n < COUTP / 16; ++n) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int co = 16 * n + P::co(g, j);
+            Real v = (Real)acc[r][n][j];
+            v = v > (Real)0 ? v : (Real)0;
+            if (z || t >= kT) v = (Real)0;
+            *reinterpret_cast<S*>(X + xoff<P, NQ>(slot, t, co / P::EPC) + (co % P::EPC) * (int)sizeof(S)) = (S)v;
+          }
         }
       }
     }
@@ -538,7 +577,7 @@ struct DLds {
   __device__ typename P::DV afrag(int n, int kc, int lane, int g) const {
     return *reinterpret_cast<const half8*>(base + lds_off<NQ>(n, lane & 15, kc * 4 + g));
   }
-  __device__ float bias(int co) const { return bias_p[co]; }
+  __device__ typename P::Acc bias_acc(int n, int g) const { return P::bias_acc(bias_p, n, g); }
 };
 template <class P, int CINP>
 struct DGlb {
@@ -546,7 +585,7 @@ struct DGlb {
   __device__ typename P::DV afrag(int n, int kc, int lane, int g) const {
     return P::ld_w(w.w + (16 * n + (lane & 15)) * CINP + kc * P::KC + g * P::CPL);
   }
-  __device__ typename P::BT bias(int co) const { return w.b[co]; }
+  __device__ typename P::Acc bias_acc(int n, int g) const { return P::bias_acc(w.b, n, g); }
 };
 
 // Stage a dense layer (P16) at `dst` (W^T image, K permuted on the host) and its bias at
@@ -568,6 +607,7 @@ template <class P, int NT>
 struct CFrag {
   static constexpr int NKC = NT * 16 / P::KC;
   typename P::DV b[NKC];
+  __device__ CFrag() {}
   __device__ CFrag(const typename P::Real (&v)[NT][4]) {
     if constexpr (P::KC == 32) {
 #pragma unroll
@@ -583,20 +623,30 @@ struct CFrag {
   }
 };
 
-template <class P, int NT, int COUTP, class WS>
-__device__ __forceinline__ void dense_c(const CFrag<P, NT>& in, const WS& ws, int lane, int g,
-                                        typename P::Real (&out)[COUTP / 16][4], bool relu) {
+// Dense layer over NR rows at once: every A fragment and bias tile is loaded once and
+// reused by the NR rows' MFMAs (the rows are independent chains).
+template <class P, int NT, int COUTP, int NR, class WS>
+__device__ __forceinline__ void dense_rows(const CFrag<P, NT> (&in)[NR], const WS& ws, int lane, int g,
+                                           typename P::Real (&out)[NR][COUTP / 16][4], bool relu) {
   using Real = typename P::Real;
+  constexpr int NKC = CFrag<P, NT>::NKC;
 #pragma unroll
   for (int n = 0; n < COUTP / 16; ++n) {
-    typename P::Acc acc = P::zero();
+    typename P::Acc acc[NR];
+    const typename P::Acc bn = ws.bias_acc(n, g);
 #pragma unroll
-    for (int kc = 0; kc < CFrag<P, NT>::NKC; ++kc) acc = P::mma_v(ws.afrag(n, kc, lane, g), in.b[kc], acc);
+    for (int kc = 0; kc < NKC; ++kc) {
+      const typename P::DV a = ws.afrag(n, kc, lane, g);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      Real v = (Real)acc[j] + (Real)ws.bias(16 * n + P::co(g, j));
-      out[n][j] = relu ? (v > (Real)0 ? v : (Real)0) : v;
+      for (int r = 0; r < NR; ++r) acc[r] = P::mma_v(a, in[r].b[kc], kc == 0 ? bn : acc[r]);
     }
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const Real v = (Real)acc[r][j];
+        out[r][n][j] = relu ? (v > (Real)0 ? v : (Real)0) : v;
+      }
   }
 }
 
@@ -607,11 +657,21 @@ __device__ __forceinline__ int head_w2(int h) { return head_w1(h) + 16 * 1024; }
 __device__ __forceinline__ int head_b1(int h) { return head_w1(h) + kHeadSlot; }
 __device__ __forceinline__ int head_b2(int h) { return head_b1(h) + 512; }
 
-// conv3 epilogue: new state rows (+ aggregation MLP or readouts) for R rows of a wave.
+// conv3 epilogue: new state rows (+ aggregation MLP or readouts) for the R rows of a
+// wave.  All R rows are computed unconditionally (rows past the strip or the grid hold
+// finite values from zero inputs) so the MLP chains of the rows interleave; only the
+// stores are predicated.  The skip / Var-IO partial sum is prefetched before the conv3
+// math (prefetch()), so its global latency hides behind it.
 template <class P, class WS, int CHP, int TAILM>
 struct EpiConv3 {
   using S = typename P::S;
   using Real = typename P::Real;
+  static constexpr int R = P::R;
+  static constexpr int NTS = kDSP / 16;        // state tiles (64 channels, >= 56 are 0)
+  // previous state rows, kept in storage precision (packed) until the epilogue
+  struct Pref {
+    std::conditional_t<sizeof(S) == 2, half4, Real[4]> prev[R][NTS];
+  };
   const BlockParams<P>* prm;
   char* X;
   char* WB;
@@ -619,6 +679,34 @@ struct EpiConv3 {
   int b, u, f_start, pos_hi, mode;   // mode 0: update (+skip), 1: init (x wm, Var-IO accumulate)
   Real wm;
   bool first;
+
+  __device__ bool row_ok(int p, int t) const { return p < pos_hi && f_start + p < prm->a.F && t < kT; }
+
+  __device__ void prefetch(Pref& pf, int p0, int t, int g) const {
+    const auto& a = prm->a;
+    const bool need = mode == 0 || !first;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool ok = need && row_ok(p0 + r, t);
+      const size_t off = srow(b, u, ok ? f_start + p0 + r : 0, ok ? t : 0, a.U, a.F);
+      const S* src = (mode == 0 ? a.s_in : a.s_out) + off;
+#pragma unroll
+      for (int n = 0; n < NTS; ++n) {
+        if constexpr (sizeof(S) == 2) {
+          const int c0 = 16 * n + 4 * g;
+          half4 h4 = half4{0, 0, 0, 0};
+          if (ok && c0 < kDS) h4 = *reinterpret_cast<const half4*>(src + c0);
+          pf.prev[r][n] = h4;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int co = 16 * n + P::co(g, j);
+            pf.prev[r][n][j] = (ok && co < kDS) ? (Real)src[co] : (Real)0;
+          }
+        }
+      }
+    }
+  }
 
   __device__ void pre() const {
     if constexpr (P::WLDS) {
@@ -637,145 +725,179 @@ struct EpiConv3 {
     }
   }
 
-  template <int NH2, class W1, class W2>
-  __device__ __forceinline__ void head(const CFrag<P, kDSP / 16>& sb, const W1& w1, const W2& w2, int lane,
-                                       int g, Real (&o)[NH2][4]) const {
-    Real hdn[kHID / 16][4];
-    dense_c<P, kDSP / 16, kHID>(sb, w1, lane, g, hdn, true);
-    CFrag<P, kHID / 16> hb(hdn);
-    dense_c<P, kHID / 16, NH2 * 16>(hb, w2, lane, g, o, false);
+  // store NT16 tiles of f32 outputs for one row: channel co = 16 n + P::co(g, j) < nvalid
+  template <int NT16>
+  __device__ __forceinline__ void store_f32(float* dst, const Real (&o)[NT16][4], int g, int nvalid) const {
+#pragma unroll
+    for (int n = 0; n < NT16; ++n) {
+      if constexpr (sizeof(S) == 2) {
+        const int c0 = 16 * n + 4 * g;
+        if (c0 + 3 < nvalid && (nvalid & 3) == 0) {
+          *reinterpret_cast<floatx4*>(dst + c0) = floatx4{(float)o[n][0], (float)o[n][1], (float)o[n][2], (float)o[n][3]};
+          continue;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = 16 * n + P::co(g, j);
+        if (co < nvalid) dst[co] = (float)o[n][j];
+      }
+    }
   }
 
-  __device__ void operator()(const typename P::Acc (&acc)[P::R][kDSP / 16], int p0, int t, int g) const {
+  template <int NO, int RB, class W1, class W2>
+  __device__ __forceinline__ void head_rows(const CFrag<P, NTS> (&sb)[RB], const W1& w1, const W2& w2, int lane,
+                                            int g, Real (&o)[RB][NO][4]) const {
+    Real hdn[RB][kHID / 16][4];
+    dense_rows<P, NTS, kHID, RB>(sb, w1, lane, g, hdn, true);
+    CFrag<P, kHID / 16> hb[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) hb[r] = CFrag<P, kHID / 16>(hdn[r]);
+    dense_rows<P, kHID / 16, NO * 16, RB>(hb, w2, lane, g, o, false);
+  }
+
+  __device__ void operator()(const typename P::Acc (&acc)[R][NTS], const Pref& pf, int p0, int t, int g) const {
     const auto& a = prm->a;
     const int F = a.F, U = a.U;
     const int lane = threadIdx.x & 63;
-    const bool tv = t < kT && !(NRX_ABLATE & 16);
+    // ---- new state rows s (C layout, channels >= 56 forced to 0), rounded to S
+    Real sv[R][NTS][4];
 #pragma unroll
-    for (int r = 0; r < P::R; ++r) {
-      const int p = p0 + r;
-      const int f = f_start + p;
-      if (p >= pos_hi || f >= F) continue;     // wave-uniform
-      const size_t off = srow(b, u, f, tv ? t : 0, U, F);
-      // ---- new state s (C layout, channels >= 56 forced to 0)
-      Real sv[kDSP / 16][4];
+    for (int r = 0; r < R; ++r)
 #pragma unroll
-      for (int n = 0; n < kDSP / 16; ++n) {
-        Real prev[4] = {0, 0, 0, 0};
-        const int c0 = 16 * n + P::co(g, 0);
-        if (tv && (mode == 0 || !first)) {
-          const S* src = (mode == 0 ? a.s_in : a.s_out) + off;
-          if constexpr (sizeof(S) == 2) {
-            if (c0 < kDS) {
-              const half4 h4 = *reinterpret_cast<const half4*>(src + c0);
-#pragma unroll
-              for (int j = 0; j < 4; ++j) prev[j] = (Real)h4[j];
-            }
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int co = 16 * n + P::co(g, j);
-              if (co < kDS) prev[j] = (Real)src[co];
-            }
-          }
-        }
+      for (int n = 0; n < NTS; ++n)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int co = 16 * n + P::co(g, j);
-          Real v = (Real)acc[r][n][j] + (Real)ws.bias(co);
+          Real v = (Real)acc[r][n][j];
           if (mode == 1) v *= wm;
-          v += prev[j];
+          v += (Real)pf.prev[r][n][j];
           if (co >= kDS) v = 0;
-          sv[n][j] = (Real)(S)v;               // the state is stored (and consumed) in S
+          sv[r][n][j] = (Real)(S)v;
         }
-      }
-      if (TAILM != TAIL_READOUT && tv) {
-        S* dst = a.s_out + off;
+    size_t off[R];
+    bool ok[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      ok[r] = row_ok(p0 + r, t) && !(NRX_ABLATE & 16);
+      off[r] = srow(b, u, ok[r] ? f_start + p0 + r : 0, ok[r] ? t : 0, U, F);
+    }
+    if constexpr (TAILM != TAIL_READOUT) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (!ok[r]) continue;
+        S* dst = a.s_out + off[r];
         if constexpr (sizeof(S) == 2) {
 #pragma unroll
-          for (int n = 0; n < kDSP / 16; ++n) {
+          for (int n = 0; n < NTS; ++n) {
             const int c0 = 16 * n + 4 * g;
             if (c0 < kDS)
               *reinterpret_cast<half4*>(dst + c0) =
-                  half4{(S)sv[n][0], (S)sv[n][1], (S)sv[n][2], (S)sv[n][3]};
+                  half4{(S)sv[r][n][0], (S)sv[r][n][1], (S)sv[r][n][2], (S)sv[r][n][3]};
           }
         } else {
 #pragma unroll
-          for (int n = 0; n < kDSP / 16; ++n)
+          for (int n = 0; n < NTS; ++n)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int co = 16 * n + P::co(g, j);
-              if (co < kDS) dst[co] = (S)sv[n][j];
+              if (co < kDS) dst[co] = (S)sv[r][n][j];
             }
         }
       }
-      if constexpr (TAILM == TAIL_NONE) continue;
-      CFrag<P, kDSP / 16> sb(sv);
-      if constexpr (TAILM == TAIL_AGG) {
-        // sp_u = act_u * (W2 relu(W1 s + b1) + b2)  -> a_out (combined by the tail)
-        Real hdn[kAGG / 16][4], sp[kDSP / 16][4];
-        const Real act = (Real)a.active[(size_t)b * U + u];
-        if constexpr (P::WLDS) {
-          DLds<P, kDSP> w1{WB + 16 * 1024, reinterpret_cast<const float*>(WB + kWTailBias)};
-          DLds<P, kAGG> w2{WB + 24 * 1024, reinterpret_cast<const float*>(WB + kWTailBias + kAGG * 4)};
-          dense_c<P, kDSP / 16, kAGG>(sb, w1, lane, g, hdn, true);
-          CFrag<P, kAGG / 16> hb(hdn);
-          dense_c<P, kAGG / 16, kDSP>(hb, w2, lane, g, sp, false);
-        } else {
-          dense_c<P, kDSP / 16, kAGG>(sb, DGlb<P, kDSP>{prm->agg[0]}, lane, g, hdn, true);
-          CFrag<P, kAGG / 16> hb(hdn);
-          dense_c<P, kAGG / 16, kDSP>(hb, DGlb<P, kAGG>{prm->agg[1]}, lane, g, sp, false);
-        }
-        if (tv) {
-          S* dst = a.a_out + off;
+    }
+    if constexpr (TAILM == TAIL_NONE) return;
+    CFrag<P, NTS> sb[R];
 #pragma unroll
-          for (int n = 0; n < kDSP / 16; ++n)
+    for (int r = 0; r < R; ++r) sb[r] = CFrag<P, NTS>(sv[r]);
+    if constexpr (TAILM == TAIL_AGG) {
+      // sp_u = act_u * (W2 relu(W1 s + b1) + b2)  -> a_out (combined by the tail)
+      Real hdn[R][kAGG / 16][4], sp[R][NTS][4];
+      const Real act = (Real)a.active[(size_t)b * U + u];
+      CFrag<P, kAGG / 16> hb[R];
+      if constexpr (P::WLDS) {
+        DLds<P, kDSP> w1{WB + 16 * 1024, reinterpret_cast<const float*>(WB + kWTailBias)};
+        DLds<P, kAGG> w2{WB + 24 * 1024, reinterpret_cast<const float*>(WB + kWTailBias + kAGG * 4)};
+        dense_rows<P, NTS, kAGG, R>(sb, w1, lane, g, hdn, true);
+#pragma unroll
+        for (int r = 0; r < R; ++r) hb[r] = CFrag<P, kAGG / 16>(hdn[r]);
+        dense_rows<P, kAGG / 16, kDSP, R>(hb, w2, lane, g, sp, false);
+      } else {
+        dense_rows<P, NTS, kAGG, R>(sb, DGlb<P, kDSP>{prm->agg[0]}, lane, g, hdn, true);
+#pragma unroll
+        for (int r = 0; r < R; ++r) hb[r] = CFrag<P, kAGG / 16>(hdn[r]);
+        dense_rows<P, kAGG / 16, kDSP, R>(hb, DGlb<P, kAGG>{prm->agg[1]}, lane, g, sp, false);
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (!ok[r]) continue;
+        S* dst = a.a_out + off[r];
+        if constexpr (sizeof(S) == 2) {
+#pragma unroll
+          for (int n = 0; n < NTS; ++n) {
+            const int c0 = 16 * n + 4 * g;
+            if (c0 < kDS)
+              *reinterpret_cast<half4*>(dst + c0) = half4{(S)(sp[r][n][0] * act), (S)(sp[r][n][1] * act),
+                                                          (S)(sp[r][n][2] * act), (S)(sp[r][n][3] * act)};
+          }
+        } else {
+#pragma unroll
+          for (int n = 0; n < NTS; ++n)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int co = 16 * n + P::co(g, j);
-              if (co < kDS) dst[co] = (S)(sp[n][j] * act);
+              if (co < kDS) dst[co] = (S)(sp[r][n][j] * act);
             }
         }
-      } else {
-        // readouts: LLR head(s) then ChEst
+      }
+    } else {
+      // readouts: LLR head(s) then ChEst, RB rows at a time
+      constexpr int RB = R >= 2 ? 2 : 1;
+#pragma unroll
+      for (int r0 = 0; r0 < R; r0 += RB) {
+        CFrag<P, NTS> sbr[RB];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) sbr[r] = sb[r0 + r];
         for (int hh = 0; hh <= a.H; ++hh) {
           const bool ch = hh == a.H;
           if (ch && !a.h_ref) break;
           if (!ch) {
-            Real o[1][4];
+            Real o[RB][1][4];
             if constexpr (P::WLDS) {
-              head<1>(sb, DLds<P, kDSP>{X + head_w1(hh), reinterpret_cast<const float*>(X + head_b1(hh))},
-                      DLds<P, kHID>{X + head_w2(hh), reinterpret_cast<const float*>(X + head_b2(hh))}, lane, g, o);
+              head_rows<1, RB>(sbr, DLds<P, kDSP>{X + head_w1(hh), reinterpret_cast<const float*>(X + head_b1(hh))},
+                               DLds<P, kHID>{X + head_w2(hh), reinterpret_cast<const float*>(X + head_b2(hh))},
+                               lane, g, o);
             } else {
-              head<1>(sb, DGlb<P, kDSP>{prm->llr[hh][0]}, DGlb<P, kHID>{prm->llr[hh][1]}, lane, g, o);
+              head_rows<1, RB>(sbr, DGlb<P, kDSP>{prm->llr[hh][0]}, DGlb<P, kHID>{prm->llr[hh][1]}, lane, g, o);
             }
-            if (tv) {
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+              if (!ok[r0 + r]) continue;
+              const int f = f_start + p0 + r0 + r;
               float* dst = a.llr + ((((size_t)hh * a.B + b) * U + u) * F + f) * kT * a.bits_max + t * a.bits_max;
+              // head bits beyond head_bits[hh] (masking: sliced later) are written as 0
 #pragma unroll
               for (int j = 0; j < 4; ++j) {
                 const int co = P::co(g, j);
-                if (co < a.bits_max) dst[co] = co < a.head_bits[hh] ? (float)o[0][j] : 0.f;
+                if (co < a.bits_max) dst[co] = co < a.head_bits[hh] ? (float)o[r][0][j] : 0.f;
               }
             }
           } else {
-            Real o[CHP / 16][4];
+            Real o[RB][CHP / 16][4];
             if constexpr (P::WLDS) {
-              head<CHP / 16>(sb, DLds<P, kDSP>{X + head_w1(hh), reinterpret_cast<const float*>(X + head_b1(hh))},
-                             DLds<P, kHID>{X + head_w2(hh), reinterpret_cast<const float*>(X + head_b2(hh))}, lane,
-                             g, o);
+              head_rows<CHP / 16, RB>(sbr,
+                                      DLds<P, kDSP>{X + head_w1(hh), reinterpret_cast<const float*>(X + head_b1(hh))},
+                                      DLds<P, kHID>{X + head_w2(hh), reinterpret_cast<const float*>(X + head_b2(hh))},
+                                      lane, g, o);
             } else {
-              head<CHP / 16>(sb, DGlb<P, kDSP>{prm->chest[0]}, DGlb<P, kHID>{prm->chest[1]}, lane, g, o);
+              head_rows<CHP / 16, RB>(sbr, DGlb<P, kDSP>{prm->chest[0]}, DGlb<P, kHID>{prm->chest[1]}, lane, g, o);
             }
-            if (tv) {
-              const int A2 = 2 * a.A;
-              float* dst = a.h_ref + ((((size_t)b * U + u) * F + f) * kT + t) * A2;
+            const int A2 = 2 * a.A;
 #pragma unroll
-              for (int n = 0; n < CHP / 16; ++n)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                  const int co = 16 * n + P::co(g, j);
-                  if (co < A2) dst[co] = (float)o[n][j];
-                }
+            for (int r = 0; r < RB; ++r) {
+              if (!ok[r0 + r]) continue;
+              const int f = f_start + p0 + r0 + r;
+              store_f32<CHP / 16>(a.h_ref + ((((size_t)b * U + u) * F + f) * kT + t) * A2, o[r], g, A2);
             }
           }
         }
@@ -819,6 +941,15 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
   char* X = smem;
   char* WB = smem + R0 * slot_pitch<P>();
   const Real ns = (Real)a.norm[b];
+  if constexpr (sizeof(S) == 2 && CINP < kHID) {
+    // pad symbols t = 14, 15 of the 128-channel layout the conv layers write in place:
+    // zero once (the z image below occupies the first CINP*32 bytes of each slot)
+    constexpr int NQ = kHID * (int)sizeof(S) / 16;
+    for (int idx = threadIdx.x; idx < R0 * 2 * NQ; idx += 512) {
+      const int q = idx % NQ, tt = kT + (idx / NQ) % 2, lf = idx / (2 * NQ);
+      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(lf, tt, q)) = intx4{0, 0, 0, 0};
+    }
+  }
   constexpr int NZ = R0 * kTP * CINP;
   constexpr int BATCH = 32;
   for (int base = 0; base < NZ; base += 512 * BATCH) {
@@ -938,44 +1069,52 @@ __device__ __forceinline__ void tail_combine(const BlockParams<P>& prm, int b, i
   const int f0 = strip * P::FO;
   const int f1 = f0 + P::FO < F ? f0 + P::FO : F;
   const int nitem = (f1 - f0) * kT * QS;
-  constexpr int IB = 2;
+  // two passes over the users (sum, then write): registers independent of U; the second
+  // pass re-reads the rows from L2
+  constexpr int IB = 4;
   for (int base = threadIdx.x; base < nitem; base += 512 * IB) {
-    intx4 v[IB][kMaxUsers];
+    Real sum[IB][P::EPC];
 #pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      const int idx = base + i * 512;
+    for (int i = 0; i < IB; ++i)
 #pragma unroll
-      for (int uu = 0; uu < kMaxUsers; ++uu)
-        if (uu < U && idx < nitem) {
-          const int q = idx % QS, rowi = idx / QS;
-          v[i][uu] = *reinterpret_cast<const intx4*>(a.a_out + srow(b, uu, f0, 0, U, F) + (size_t)rowi * kDS + q * P::EPC);
-        }
+      for (int e = 0; e < P::EPC; ++e) sum[i][e] = 0;
+    for (int uu = 0; uu < U; ++uu) {
+      intx4 v[IB];
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        const int idx = base + i * 512;
+        v[i] = intx4{0, 0, 0, 0};
+        if (idx < nitem)
+          v[i] = *reinterpret_cast<const intx4*>(a.a_out + srow(b, uu, f0, 0, U, F) + (size_t)(idx / QS) * kDS +
+                                                 (idx % QS) * P::EPC);
+      }
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        const S* sv = reinterpret_cast<const S*>(&v[i]);
+#pragma unroll
+        for (int e = 0; e < P::EPC; ++e) sum[i][e] += (Real)sv[e];
+      }
     }
+    for (int uu = 0; uu < U; ++uu) {
+      intx4 v[IB];
 #pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      const int idx = base + i * 512;
-      if (idx >= nitem) continue;
-      const int q = idx % QS, rowi = idx / QS;
-      Real sum[P::EPC];
+      for (int i = 0; i < IB; ++i) {
+        const int idx = base + i * 512;
+        if (idx < nitem)
+          v[i] = *reinterpret_cast<const intx4*>(a.a_out + srow(b, uu, f0, 0, U, F) + (size_t)(idx / QS) * kDS +
+                                                 (idx % QS) * P::EPC);
+      }
 #pragma unroll
-      for (int e = 0; e < P::EPC; ++e) sum[e] = 0;
+      for (int i = 0; i < IB; ++i) {
+        const int idx = base + i * 512;
+        if (idx >= nitem) continue;
+        const S* sv = reinterpret_cast<const S*>(&v[i]);
+        S o[P::EPC];
 #pragma unroll
-      for (int uu = 0; uu < kMaxUsers; ++uu)
-        if (uu < U) {
-          const S* sv = reinterpret_cast<const S*>(&v[i][uu]);
-#pragma unroll
-          for (int e = 0; e < P::EPC; ++e) sum[e] += (Real)sv[e];
-        }
-#pragma unroll
-      for (int uu = 0; uu < kMaxUsers; ++uu)
-        if (uu < U) {
-          const S* sv = reinterpret_cast<const S*>(&v[i][uu]);
-          S o[P::EPC];
-#pragma unroll
-          for (int e = 0; e < P::EPC; ++e) o[e] = (S)((sum[e] - (Real)sv[e]) * p);
-          *reinterpret_cast<intx4*>(a.a_out + srow(b, uu, f0, 0, U, F) + (size_t)rowi * kDS + q * P::EPC) =
-              *reinterpret_cast<const intx4*>(o);
-        }
+        for (int e = 0; e < P::EPC; ++e) o[e] = (S)((sum[i][e] - (Real)sv[e]) * p);
+        *reinterpret_cast<intx4*>(a.a_out + srow(b, uu, f0, 0, U, F) + (size_t)(idx / QS) * kDS + (idx % QS) * P::EPC) =
+            *reinterpret_cast<const intx4*>(o);
+      }
     }
   }
 }
