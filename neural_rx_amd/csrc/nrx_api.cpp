@@ -371,7 +371,6 @@ static void fill_args(FwdArgs<WT, BT, S>& a, const nrx_handle* h, const nrx_io* 
   a.s_out = (S*)p;
   a.a = (S*)(p + 3 * sb);
   a.a_out = (S*)(p + 2 * sb);
-  a.counters = (unsigned*)(p + 4 * sb);
 }
 
 
@@ -437,9 +436,7 @@ int nrx_workspace_size(const nrx_handle* h, const nrx_shape* shape, int32_t prec
   if (rc) return rc;
   if (precision != NRX_PREC_F16 && precision != NRX_PREC_F32X)
     return fail(NRX_ERR_INVALID_ARG, "unknown precision");
-  const int strips = (shape->num_subcarriers + strip_width(precision) - 1) / strip_width(precision);
-  *bytes = align256((size_t)shape->batch * sizeof(double)) + 4 * state_bytes(shape, precision) +
-           align256((size_t)(kMaxIt + 1) * shape->batch * strips * sizeof(unsigned));
+  *bytes = align256((size_t)shape->batch * sizeof(double)) + 4 * state_bytes(shape, precision);
   return NRX_OK;
 }
 

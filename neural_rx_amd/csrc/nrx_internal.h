@@ -23,6 +23,7 @@ constexpr int kAGG = 64;      // aggregation hidden width
 constexpr int kUPD_CINP = 128;  // [a, s, pe] = 114 -> 128
 constexpr int kMaxInit = 8;
 constexpr int kMaxIt = 8;
+constexpr int kInlineUsers = 4;  // users whose leave-one-out combine the update z-load forms
 constexpr int kMaxHeads = 8;
 constexpr int kMaxUsers = 16;
 constexpr int kHalo = 3;      // 3 stacked 3x3 convs per block
@@ -71,7 +72,6 @@ struct FwdArgs {
   S* s_out;
   S* a;                            // aggregate read by this update
   S* a_out;                        // aggregate written by the tail
-  unsigned* counters;              // [num_it + 1][B][strips] arrival tickets
 };
 
 // Optional per-kernel timing (nrx_profile_enable): events recorded around each launch on

@@ -31,6 +31,7 @@
 //   P64: f32 storage, f64 depthwise, mfma_f64_16x16x4f64 (parity mode).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 #include <utility>
@@ -47,8 +48,9 @@ namespace nrx {
 #ifdef NRX_STAMPS
 // diagnostic builds only: s_memtime per phase, wave 0 lane 0 of each workgroup
 __device__ unsigned long long g_nrx_stamps[4096][8];
+__device__ int g_nrx_stamp_on;   // set by the host for the k_update launch to record
 __device__ __forceinline__ void stamp(int k) {
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && g_nrx_stamp_on) {
     const int wg = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     if (wg < 4096) g_nrx_stamps[wg][k] = __builtin_amdgcn_s_memtime();
   }
@@ -58,6 +60,7 @@ __device__ __forceinline__ void stamp(int) {}
 #endif
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half2 __attribute__((ext_vector_type(2)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef double doublex4 __attribute__((ext_vector_type(4)));
@@ -71,6 +74,19 @@ __device__ __forceinline__ int dpp_shr1(int v) {
 }
 __device__ __forceinline__ int dpp_shl1(int v) {
   return __builtin_amdgcn_update_dpp(0, v, 0x101, 0xf, 0xf, true);
+}
+
+// d += x(t -+ 1) * w on packed halves: v_pk_fmac_f16 with a DPP row shift on x (the
+// lane without a source reads 0: bound_ctrl).  The compiler's hazard recognizer covers
+// inline asm (it inserts the VALU-write -> DPP-read wait states).
+__device__ __forceinline__ void fmac_shr(half2& d, half2 x, half2 w) {
+  asm("v_pk_fmac_f16_dpp %0, %1, %2 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(d) : "v"(x), "v"(w));
+}
+__device__ __forceinline__ void fmac_shl(half2& d, half2 x, half2 w) {
+  asm("v_pk_fmac_f16_dpp %0, %1, %2 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(d) : "v"(x), "v"(w));
+}
+__device__ __forceinline__ half2 h2(half8 v, int k) {
+  return half2{v[2 * k], v[2 * k + 1]};
 }
 
 struct P16 {
@@ -100,6 +116,23 @@ struct P16 {
   // accumulator-layout bias of output tile n (C operand of the first MFMA of a chain)
   __device__ static Acc bias_acc(const float* b, int n, int g) {
     return *reinterpret_cast<const floatx4*>(b + 16 * n + 4 * g);
+  }
+  // depthwise 3x3 of one output row from its three input rows (x0 = f-1, x1 = f, x2 = f+1);
+  // tap = i*3 + j, i along subcarriers, j along symbols (j = 0 reads t-1).
+  __device__ static DV dw_row(DV x0, DV x1, DV x2, const DV (&w)[9]) {
+    const DV c = w[1] * x0 + w[4] * x1 + w[7] * x2;
+    half2 d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      d[k] = h2(c, k);
+      fmac_shr(d[k], h2(x0, k), h2(w[0], k));
+      fmac_shr(d[k], h2(x1, k), h2(w[3], k));
+      fmac_shr(d[k], h2(x2, k), h2(w[6], k));
+      fmac_shl(d[k], h2(x0, k), h2(w[2], k));
+      fmac_shl(d[k], h2(x1, k), h2(w[5], k));
+      fmac_shl(d[k], h2(x2, k), h2(w[8], k));
+    }
+    return DV{d[0][0], d[0][1], d[1][0], d[1][1], d[2][0], d[2][1], d[3][0], d[3][1]};
   }
   __device__ static DV shr(DV v) {
     intx4 x = __builtin_bit_cast(intx4, v);
@@ -149,6 +182,12 @@ struct P64 {
     return c;
   }
   __device__ static int co(int g, int j) { return g + 4 * j; }
+  __device__ static DV dw_row(DV x0, DV x1, DV x2, const DV (&w)[9]) {
+    const DV cm = w[0] * x0 + w[3] * x1 + w[6] * x2;
+    const DV c0 = w[1] * x0 + w[4] * x1 + w[7] * x2;
+    const DV cp = w[2] * x0 + w[5] * x1 + w[8] * x2;
+    return c0 + shr(cm) + shl(cp);
+  }
   __device__ static Acc bias_acc(const double* b, int n, int g) {
     return Acc{b[16 * n + g], b[16 * n + g + 4], b[16 * n + g + 8], b[16 * n + g + 12]};
   }
@@ -293,13 +332,7 @@ __device__ __forceinline__ void conv_chunk(const char* X, const int (&rb)[P::R +
   for (int k = 0; k < 9; ++k) w[k] = ws.dwv(k, kc, g);
   DV d[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    // column sums per symbol offset dt = j - 1 (tap = i*3 + j, i along subcarriers)
-    const DV cm = w[0] * xs[r] + w[3] * xs[r + 1] + w[6] * xs[r + 2];
-    const DV c0 = w[1] * xs[r] + w[4] * xs[r + 1] + w[7] * xs[r + 2];
-    const DV cp = w[2] * xs[r] + w[5] * xs[r + 1] + w[8] * xs[r + 2];
-    d[r] = c0 + P::shr(cm) + P::shl(cp);
-  }
+  for (int r = 0; r < R; ++r) d[r] = P::dw_row(xs[r], xs[r + 1], xs[r + 2], w);
 #pragma unroll
   for (int n = 0; n < COUTP / 16; ++n) {
     const DV a = ws.afrag(n, kc, lane, g);
@@ -515,7 +548,7 @@ struct BlockParams {
   DenseW<typename P::WT, typename P::BT> chest[2];
   int tail;                                              // TAIL_AGG / TAIL_READOUT / TAIL_NONE
   int m;                                                 // init: which StateInit (Var-IO)
-  unsigned* counters;                                    // [B][strips] arrival tickets (agg tail)
+  int inline_combine;                                    // U <= kInlineUsers: z-load forms a
 };
 
 template <class P>
@@ -1002,44 +1035,92 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
   const int f_start = f0 - kHalo;
   char* X = smem;
   char* WB = smem + R0 * slot_pitch<P>();
-  // z chunks: [0,QS) <- a, [QS,2QS) <- s, 2QS <- pe (2 values), rest 0.  All global
-  // loads of a thread are issued first, then the LDS stores.
-  constexpr int NZ = R0 * kTP * NQ;
-  constexpr int PER = (NZ + 511) / 512;
-  intx4 v[PER];
+  // z chunks: [0,QS) <- a, [QS,2QS) <- s, 2QS <- pe (2 values), rest 0.
+  // a_u = (sum_u' sp_u' - sp_u) * p is formed here from the producer's act*sp rows when
+  // U <= kInlineUsers (AggregateUserStates' leave-one-out mean, neural_rx.py:191-204);
+  // otherwise k_combine already wrote a_u in place.  All global loads of a thread are
+  // issued first, then the LDS stores.
+  using Real = typename P::Real;
+  constexpr int NA = R0 * kTP * QS;                    // a chunks
+  constexpr int NO = R0 * kTP * (NQ - QS);             // s / pe / pad chunks
+  constexpr int PA = (NA + 511) / 512, PO = (NO + 511) / 512;
+  const bool inl = prm.inline_combine != 0;
+  intx4 va[PA][kInlineUsers];
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
+  for (int i = 0; i < PA; ++i) {
     const int idx = threadIdx.x + i * 512;
-    v[i] = intx4{0, 0, 0, 0};
-    if (idx < NZ) {
-      const int q = idx % NQ;
-      const int tt = (idx / NQ) % kTP;
-      const int lf = idx / (NQ * kTP);
-      const int f = f_start + lf;
-      if (!(NRX_ABLATE & 2) && f >= 0 && f < F && tt < kT) {
-        const size_t row = srow(b, u, f, tt, U, F);
-        if (q < QS) {
-          v[i] = *reinterpret_cast<const intx4*>(a.a + row + q * P::EPC);
-        } else if (q < 2 * QS) {
-          v[i] = *reinterpret_cast<const intx4*>(a.s_in + row + (q - QS) * P::EPC);
-        } else if (q == 2 * QS) {
-          const float* pp = a.pe + (((size_t)u * F + f) * kT + tt) * 2;
-          S pe2[P::EPC] = {};
-          pe2[0] = (S)pp[0];
-          pe2[1] = (S)pp[1];
-          v[i] = *reinterpret_cast<const intx4*>(pe2);
-        }
+    const int rowi = idx / QS, q = idx % QS;
+    const int tt = rowi % kTP, lf = rowi / kTP;
+    const int f = f_start + lf;
+    const bool ok = !(NRX_ABLATE & 2) && idx < NA && f >= 0 && f < F && tt < kT;
+#pragma unroll
+    for (int uu = 0; uu < kInlineUsers; ++uu) {
+      va[i][uu] = intx4{0, 0, 0, 0};
+      if (ok && uu < (inl ? U : 1))
+        va[i][uu] = *reinterpret_cast<const intx4*>(a.a + srow(b, inl ? uu : u, f, tt, U, F) + q * P::EPC);
+    }
+  }
+  intx4 vo[PO];
+#pragma unroll
+  for (int i = 0; i < PO; ++i) {
+    const int idx = threadIdx.x + i * 512;
+    const int rowi = idx / (NQ - QS), q = QS + idx % (NQ - QS);
+    const int tt = rowi % kTP, lf = rowi / kTP;
+    const int f = f_start + lf;
+    vo[i] = intx4{0, 0, 0, 0};
+    if (!(NRX_ABLATE & 2) && idx < NO && f >= 0 && f < F && tt < kT) {
+      const size_t row = srow(b, u, f, tt, U, F);
+      if (q < 2 * QS) {
+        vo[i] = *reinterpret_cast<const intx4*>(a.s_in + row + (q - QS) * P::EPC);
+      } else if (q == 2 * QS) {
+        const float* pp = a.pe + (((size_t)u * F + f) * kT + tt) * 2;
+        S pe2[P::EPC] = {};
+        pe2[0] = (S)pp[0];
+        pe2[1] = (S)pp[1];
+        vo[i] = *reinterpret_cast<const intx4*>(pe2);
       }
     }
   }
+  Real pf = 1;
+  if (inl) {
+    Real nact = 0;
+    for (int uu = 0; uu < U; ++uu) nact += (Real)a.active[(size_t)b * U + uu];
+    pf = nact - (Real)1;
+    pf = pf > (Real)0 ? (Real)1 / pf : (Real)1;
+  }
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
+  for (int i = 0; i < PA; ++i) {
     const int idx = threadIdx.x + i * 512;
-    if (idx < NZ) {
-      const int q = idx % NQ;
-      const int tt = (idx / NQ) % kTP;
-      const int lf = idx / (NQ * kTP);
-      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(lf, tt, q)) = v[i];
+    if (idx < NA) {
+      const int rowi = idx / QS, q = idx % QS;
+      intx4 out = va[i][0];
+      if (inl) {
+        Real sum[P::EPC], own[P::EPC];
+#pragma unroll
+        for (int e = 0; e < P::EPC; ++e) sum[e] = own[e] = 0;
+#pragma unroll
+        for (int uu = 0; uu < kInlineUsers; ++uu) {
+          const S* sv = reinterpret_cast<const S*>(&va[i][uu]);
+#pragma unroll
+          for (int e = 0; e < P::EPC; ++e) {
+            sum[e] += (Real)sv[e];
+            if (uu == u) own[e] = (Real)sv[e];
+          }
+        }
+        S o[P::EPC];
+#pragma unroll
+        for (int e = 0; e < P::EPC; ++e) o[e] = (S)((sum[e] - own[e]) * pf);
+        out = *reinterpret_cast<const intx4*>(o);
+      }
+      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(rowi / kTP, rowi % kTP, q)) = out;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PO; ++i) {
+    const int idx = threadIdx.x + i * 512;
+    if (idx < NO) {
+      const int rowi = idx / (NQ - QS), q = QS + idx % (NQ - QS);
+      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(rowi / kTP, rowi % kTP, q)) = vo[i];
     }
   }
   __syncthreads();
@@ -1050,104 +1131,48 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
   stamp(4);
 }
 
-// ------------------------------------------------------------------------ agg tail
-// Leave-one-out mean over users (neural_rx.py:191-204): a_u = (sum_u' sp_u' - sp_u) * p,
-// sp_u already scaled by act_u, p = 1/max(#active - 1) (1 when <= 1 active).  Run by the
-// last workgroup of the (slot, strip) to arrive; streams a_out in place.
+// ------------------------------------------------------------ user combine (U > 4)
+// Leave-one-out mean over users (neural_rx.py:191-204) in place: a_u = (sum_u' sp_u' -
+// sp_u) * p, sp_u already scaled by act_u, p = 1/max(#active - 1) (1 when <= 1 active).
+// For U <= kInlineUsers the update kernel's z-load forms a_u itself and this is not run.
+// grid = (ceil(F*14*QS / 256), B), 256 threads, one 16-byte chunk of a row per thread.
 template <class P>
-__device__ __forceinline__ void tail_combine(const BlockParams<P>& prm, int b, int strip) {
+__global__ __launch_bounds__(256) void k_combine(typename P::S* __restrict__ buf, const float* __restrict__ active,
+                                                 int U, int F) {
   using S = typename P::S;
   using Real = typename P::Real;
-  const auto& a = prm.a;
-  const int F = a.F, U = a.U;
-  Real nact = 0;
-  for (int u = 0; u < U; ++u) nact += (Real)a.active[(size_t)b * U + u];
-  Real p = nact - (Real)1;
-  p = p > (Real)0 ? p : (Real)0;
-  p = p == (Real)0 ? (Real)1 : (Real)1 / p;
   constexpr int QS = kDS / P::EPC;
-  const int f0 = strip * P::FO;
-  const int f1 = f0 + P::FO < F ? f0 + P::FO : F;
-  const int nitem = (f1 - f0) * kT * QS;
-  // two passes over the users (sum, then write): registers independent of U; the second
-  // pass re-reads the rows from L2
-  constexpr int IB = 4;
-  for (int base = threadIdx.x; base < nitem; base += 512 * IB) {
-    Real sum[IB][P::EPC];
+  const int b = blockIdx.y;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= F * kT * QS) return;
+  const size_t ustride = (size_t)F * kT * kDS;
+  S* base = buf + (size_t)b * U * ustride + (size_t)(idx / QS) * kDS + (idx % QS) * P::EPC;
+  Real nact = 0;
+  for (int u = 0; u < U; ++u) nact += (Real)active[(size_t)b * U + u];
+  Real p = nact - (Real)1;
+  p = p > (Real)0 ? (Real)1 / p : (Real)1;
+  Real sum[P::EPC];
 #pragma unroll
-    for (int i = 0; i < IB; ++i)
+  for (int e = 0; e < P::EPC; ++e) sum[e] = 0;
+  for (int u = 0; u < U; ++u) {
+    const intx4 v = *reinterpret_cast<const intx4*>(base + u * ustride);
+    const S* sv = reinterpret_cast<const S*>(&v);
 #pragma unroll
-      for (int e = 0; e < P::EPC; ++e) sum[i][e] = 0;
-    for (int uu = 0; uu < U; ++uu) {
-      intx4 v[IB];
-#pragma unroll
-      for (int i = 0; i < IB; ++i) {
-        const int idx = base + i * 512;
-        v[i] = intx4{0, 0, 0, 0};
-        if (idx < nitem)
-          v[i] = *reinterpret_cast<const intx4*>(a.a_out + srow(b, uu, f0, 0, U, F) + (size_t)(idx / QS) * kDS +
-                                                 (idx % QS) * P::EPC);
-      }
-#pragma unroll
-      for (int i = 0; i < IB; ++i) {
-        const S* sv = reinterpret_cast<const S*>(&v[i]);
-#pragma unroll
-        for (int e = 0; e < P::EPC; ++e) sum[i][e] += (Real)sv[e];
-      }
-    }
-    for (int uu = 0; uu < U; ++uu) {
-      intx4 v[IB];
-#pragma unroll
-      for (int i = 0; i < IB; ++i) {
-        const int idx = base + i * 512;
-        if (idx < nitem)
-          v[i] = *reinterpret_cast<const intx4*>(a.a_out + srow(b, uu, f0, 0, U, F) + (size_t)(idx / QS) * kDS +
-                                                 (idx % QS) * P::EPC);
-      }
-#pragma unroll
-      for (int i = 0; i < IB; ++i) {
-        const int idx = base + i * 512;
-        if (idx >= nitem) continue;
-        const S* sv = reinterpret_cast<const S*>(&v[i]);
-        S o[P::EPC];
-#pragma unroll
-        for (int e = 0; e < P::EPC; ++e) o[e] = (S)((sum[i][e] - (Real)sv[e]) * p);
-        *reinterpret_cast<intx4*>(a.a_out + srow(b, uu, f0, 0, U, F) + (size_t)(idx / QS) * kDS + (idx % QS) * P::EPC) =
-            *reinterpret_cast<const intx4*>(o);
-      }
-    }
+    for (int e = 0; e < P::EPC; ++e) sum[e] += (Real)sv[e];
   }
-}
-
-// Arrival ticket after this workgroup's stores (cdna_hip_programming.md section 6
-// Guideline 16, counter form): every workgroup publishes its rows with an agent-scope
-// release; the one drawing the last ticket acquires and combines.  Correct for any
-// placement of the user workgroups over CUs/XCDs.
-template <class P, int TAILM>
-__device__ __forceinline__ void run_tail(const BlockParams<P>& prm, char* smem, int b, int strip, int strips) {
-  if (TAILM != TAIL_AGG || (NRX_ABLATE & 8)) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // every wave's stores done
-  __syncthreads();
-  unsigned* flag = reinterpret_cast<unsigned*>(smem);
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(prm.counters + (size_t)b * strips + strip, 1u,
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned last = old == (unsigned)(prm.a.U - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
+  for (int u = 0; u < U; ++u) {
+    const intx4 v = *reinterpret_cast<const intx4*>(base + u * ustride);
+    const S* sv = reinterpret_cast<const S*>(&v);
+    S o[P::EPC];
+#pragma unroll
+    for (int e = 0; e < P::EPC; ++e) o[e] = (S)((sum[e] - (Real)sv[e]) * p);
+    *reinterpret_cast<intx4*>(base + u * ustride) = *reinterpret_cast<const intx4*>(o);
   }
-  __syncthreads();
-  const bool last = *flag != 0;
-  if (last) tail_combine<P>(prm, b, strip);
 }
 
 // StateInit_m (+ Var-IO mix: one launch per m, m > 0 accumulating) of one (slot, user,
-// strip); the last launch applies the aggregation MLP of iteration 0.  grid = (strips, U, B).
+// strip); the last launch applies the aggregation MLP of iteration 0 (stores act * sp).
+// grid = (strips, U, B).
 template <class P, int CINP, int CHP, int TAILM>
 __global__ __launch_bounds__(512) void k_init(BlockParams<P> prm) {
   using Real = typename P::Real;
@@ -1162,17 +1187,15 @@ __global__ __launch_bounds__(512) void k_init(BlockParams<P> prm) {
   // wm == 0: this MCS contributes exactly 0 * finite; the conv math is still run (the
   // m = 0 launch defines s, the last launch applies the aggregation MLP).
   init_user<P, CINP, CHP, TAILM>(prm, smem, b, u, strip, wm, m == 0);
-  run_tail<P, TAILM>(prm, smem, b, strip, gridDim.x);
 }
 
-// UpdateState of one (slot, user, strip), then the tail.  grid = (strips, U, B).
+// UpdateState of one (slot, user, strip) with the fused tail.  grid = (strips, U, B).
 template <class P, int CHP, int TAILM>
 __global__ __launch_bounds__(512) void k_update(BlockParams<P> prm) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int strip = blockIdx.x, u = blockIdx.y, b = blockIdx.z;
   stamp(0);
   update_user<P, CHP, TAILM>(prm, smem, b, u, strip);
-  run_tail<P, TAILM>(prm, smem, b, strip, gridDim.x);
   stamp(5);
 }
 
@@ -1216,12 +1239,13 @@ struct Launch {
     auto E_ = [&](int k) { if (prof) prof->end(k, st); };
     BlockParams<P> bp;
     bp.a = args;
-    {
-      // arrival tickets of the aggregation tails: zeroed on the stream every forward
-      const size_t bytes = (size_t)(num_it + 1) * args.B * strips * sizeof(unsigned);
-      hipError_t e = hipMemsetAsync(args.counters, 0, bytes, st);
-      if (e != hipSuccess) return e;
-    }
+    bp.inline_combine = args.U <= kInlineUsers;
+    // U > kInlineUsers: the leave-one-out combine runs as its own launch on the sp rows
+    auto combine = [&](typename P::S* sp) {
+      if (bp.inline_combine) return;
+      dim3 g((args.F * kT * (kDS / P::EPC) + 255) / 256, args.B);
+      k_combine<P><<<g, 256, 0, st>>>(sp, args.active, args.U, args.F);
+    };
     for (int h = 0; h < args.H; ++h) {
       bp.llr[h][0] = W.llr[h][0];
       bp.llr[h][1] = W.llr[h][1];
@@ -1232,14 +1256,12 @@ struct Launch {
     k_norm<<<args.B, 256, 0, st>>>(args.y, args.F * kT * 2 * args.A, args.norm);
     E_(K_NORM);
     // StateInit -> s_out; tail of the last StateInit launch: aggregation of iteration 0
-    const size_t ncnt = (size_t)args.B * strips;
     dim3 grid(strips, args.U, args.B);
     B_(K_INIT);
     for (int m = 0; m < args.num_init; ++m) {
       for (int l = 0; l < 3; ++l) bp.w[l] = W.init[m][l];
       bp.m = m;
       bp.tail = m == args.num_init - 1 ? TAIL_AGG : TAIL_NONE;
-      bp.counters = args.counters;
       bp.agg[0] = W.agg[0][0];
       bp.agg[1] = W.agg[0][1];
       const bool tl = bp.tail == TAIL_AGG;
@@ -1248,18 +1270,26 @@ struct Launch {
       else ch32 ? launch_init<128, 32>(grid, L, st, bp, tl) : launch_init<128, 16>(grid, L, st, bp, tl);
     }
     E_(K_INIT);
+    combine(bp.a.a_out);
     for (int i = 0; i < num_it; ++i) {
       std::swap(bp.a.s_in, bp.a.s_out);
       std::swap(bp.a.a, bp.a.a_out);
       for (int l = 0; l < 3; ++l) bp.w[l] = W.upd[i][l];
       const bool last = i == num_it - 1;
       bp.tail = last ? TAIL_READOUT : TAIL_AGG;
-      bp.counters = args.counters + (size_t)(i + 1) * ncnt;
       if (!last) {
         bp.agg[0] = W.agg[i + 1][0];
         bp.agg[1] = W.agg[i + 1][1];
       }
       B_(K_UPDATE);
+#ifdef NRX_STAMPS
+      {
+        static const int sel = getenv("NRX_STAMP_LAUNCH") ? atoi(getenv("NRX_STAMP_LAUNCH")) : 0;
+        const int on = i == sel;
+        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_nrx_stamp_on), &on, sizeof(int), 0, hipMemcpyHostToDevice, st);
+        (void)hipStreamSynchronize(st);
+      }
+#endif
       if (last) {
         if (ch32) k_update<P, 32, TAIL_READOUT><<<grid, 512, L, st>>>(bp);
         else k_update<P, 16, TAIL_READOUT><<<grid, 512, L, st>>>(bp);
@@ -1268,6 +1298,7 @@ struct Launch {
         else k_update<P, 16, TAIL_AGG><<<grid, 512, L, st>>>(bp);
       }
       E_(K_UPDATE);
+      if (!last) combine(bp.a.a_out);
     }
     return hipGetLastError();
   }

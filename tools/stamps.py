@@ -27,6 +27,7 @@ lib.nrx_debug_stamps(buf.ctypes.data, n)
 st = buf[:, :6].astype(np.int64)
 d = np.diff(st, axis=1)
 names = ["z-load", "conv1", "conv2", "conv3+epi", "tail"]
+print("k_update launch", os.environ.get("NRX_STAMP_LAUNCH", "0"))
 tot = st[:, 5] - st[:, 0]
 print("cycles per WG (mean):", tot.mean(), " start spread:", st[:, 0].max() - st[:, 0].min())
 for i, nm in enumerate(names):
