@@ -276,41 +276,72 @@ struct WGlb {
   __device__ typename P::Acc bias_acc(int n, int g) const { return P::bias_acc(w.b, n, g); }
 };
 
-// Cooperative copy of one separable layer's packed weights into the LDS image.  All
-// global loads of a thread are issued before any LDS store (a load -> wait -> store loop
-// would pay one full memory latency per chunk).
+// Cooperative copy of one separable layer's packed weights into the LDS image, split in
+// a global-load half (issued one layer ahead, so its latency hides behind the current
+// layer's math) and an LDS-store half.
 template <int CINP, int COUTP>
-__device__ __forceinline__ void stage_weights(char* wb, const SepW<_Float16, float>& w) {
-  constexpr int NQ = CINP * 2 / 16;
-  constexpr int NPW = COUTP * NQ;                 // W^T chunks
-  constexpr int NDW = 9 * NQ;                     // dw chunks
-  constexpr int NB = COUTP / 4;                   // bias chunks (4 floats)
-  constexpr int NT = 512;
-  constexpr int PER = (NPW + NT - 1) / NT;
-  const int tid = threadIdx.x;
+struct SepStage {
+  static constexpr int NQ = CINP * 2 / 16;
+  static constexpr int NPW = COUTP * NQ;                 // W^T chunks
+  static constexpr int NDW = 9 * NQ;                     // dw chunks
+  static constexpr int NB = COUTP / 4;                   // bias chunks (4 floats)
+  static constexpr int PER = (NPW + 511) / 512;
   intx4 v[PER];
+  intx4 vx;
+  __device__ void load(const SepW<_Float16, float>& w) {
+    const int tid = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int idx = tid + i * NT;
-    if (idx < NPW) {
-      const int co = idx / NQ, q = idx % NQ;
-      v[i] = *reinterpret_cast<const intx4*>(w.pw + co * CINP + q * 8);
+    for (int i = 0; i < PER; ++i) {
+      const int idx = tid + i * 512;
+      if (idx < NPW) v[i] = *reinterpret_cast<const intx4*>(w.pw + (idx / NQ) * CINP + (idx % NQ) * 8);
     }
+    vx = intx4{0, 0, 0, 0};
+    if (tid < NDW) vx = reinterpret_cast<const intx4*>(w.dw)[tid];
+    else if (tid - NDW < NB) vx = reinterpret_cast<const intx4*>(w.b)[tid - NDW];
   }
-  intx4 vd = {0, 0, 0, 0}, vb = {0, 0, 0, 0};
-  if (tid < NDW) vd = reinterpret_cast<const intx4*>(w.dw)[tid];
-  else if (tid - NDW < NB) vb = reinterpret_cast<const intx4*>(w.b)[tid - NDW];
+  __device__ void store(char* wb) const {
+    const int tid = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int idx = tid + i * NT;
-    if (idx < NPW) {
-      const int co = idx / NQ, q = idx % NQ;
-      *reinterpret_cast<intx4*>(wb + lds_off<NQ>(co >> 4, co & 15, q)) = v[i];
+    for (int i = 0; i < PER; ++i) {
+      const int idx = tid + i * 512;
+      if (idx < NPW) {
+        const int co = idx / NQ, q = idx % NQ;
+        *reinterpret_cast<intx4*>(wb + lds_off<NQ>(co >> 4, co & 15, q)) = v[i];
+      }
     }
+    if (tid < NDW) reinterpret_cast<intx4*>(wb + kWPw)[tid] = vx;
+    else if (tid - NDW < NB) reinterpret_cast<intx4*>(wb + kWPw + kWDw)[tid - NDW] = vx;
   }
-  if (tid < NDW) reinterpret_cast<intx4*>(wb + kWPw)[tid] = vd;
-  else if (tid - NDW < NB) reinterpret_cast<intx4*>(wb + kWPw + kWDw)[tid - NDW] = vb;
-}
+};
+
+// Same split for a dense layer: W^T image (K permuted on the host) + bias.
+template <int CINP, int COUTP>
+struct DenseStage {
+  static constexpr int NQ = CINP * 2 / 16;
+  static constexpr int NW = COUTP * NQ;
+  static constexpr int PER = (NW + 511) / 512;
+  intx4 v[PER];
+  float bias;
+  __device__ void load(const DenseW<_Float16, float>& w) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = threadIdx.x + i * 512;
+      if (idx < NW) v[i] = *reinterpret_cast<const intx4*>(w.w + (idx / NQ) * CINP + (idx % NQ) * 8);
+    }
+    bias = threadIdx.x < COUTP ? w.b[threadIdx.x] : 0.f;
+  }
+  __device__ void store(char* dst, float* bias_dst) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = threadIdx.x + i * 512;
+      if (idx < NW) {
+        const int co = idx / NQ, q = idx % NQ;
+        *reinterpret_cast<intx4*>(dst + lds_off<NQ>(co >> 4, co & 15, q)) = v[i];
+      }
+    }
+    if (threadIdx.x < COUTP) bias_dst[threadIdx.x] = bias;
+  }
+};
 
 // R consecutive output rows (input slots s0 .. s0+R-1, neighbours s0-1 and s0+R) of one
 // wave, all COUTP channels, bias included (it is the C operand of the first K chunk).
@@ -370,9 +401,9 @@ __device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int
 // round computes into registers, then (after a barrier) hands the accumulators to `epi`,
 // which may overwrite input slots of rows this round consumed (in-place layers: the
 // output of position p goes to slot p - in_off - 1, which no later round reads).
-template <class P, int CINP, int COUTP, class WS, class Epi>
+template <class P, int CINP, int COUTP, class WS, class Epi, class Post>
 __device__ __forceinline__ void conv_layer(const char* X, int nslots, int in_off, int pos_lo,
-                                           int pos_hi, const WS& ws, Epi&& epi) {
+                                           int pos_hi, const WS& ws, Epi&& epi, Post&& post_math) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int t = lane & 15, g = lane >> 4;
   for (int base = pos_lo; base < pos_hi; base += 8 * P::R) {
@@ -392,6 +423,7 @@ __device__ __forceinline__ void conv_layer(const char* X, int nslots, int in_off
       }
     }
     __syncthreads();
+    if (base == pos_lo) post_math();   // all threads: this layer's weights are dead (P16)
     epi.pre();                       // all threads (e.g. stage tail weights into X)
     if (act) epi(acc, pf, p0, t, g);
     __syncthreads();
@@ -563,42 +595,22 @@ __device__ __forceinline__ size_t srow(int b, int u, int f, int t, int U, int F)
   return ((((size_t)b * U + u) * F + f) * kT + t) * kDS;
 }
 
-// Runs one separable layer of a block over the strip: stage weights (P16), then
-// conv_layer with the given epilogue.  `extra_stage` runs with the weight staging.
-template <class P, int CINP, int COUTP, class Epi, class Extra>
-__device__ __forceinline__ void strip_layer(char* X, char* WB, const SepW<typename P::WT, typename P::BT>& w,
-                                            int in_off, int pos_lo, int pos_hi, Epi&& epi_of,
-                                            Extra&& extra_stage) {
+// Runs one separable layer of a block over the strip.  P16: the layer's weights are
+// already in the LDS image WB (staged by the previous phase); `post` runs after the math.
+template <class P, int CINP, int COUTP, class Epi, class Post>
+__device__ __forceinline__ void run_layer(char* X, char* WB, const SepW<typename P::WT, typename P::BT>& w,
+                                          int in_off, int pos_lo, int pos_hi, Epi&& epi_of, Post&& post) {
   constexpr int R0 = strip_slots<P>();
   if constexpr (P::WLDS) {
-    if constexpr (!(NRX_ABLATE & 4)) stage_weights<CINP, COUTP>(WB, w);
-    extra_stage();
-    __syncthreads();
     WLds<P, CINP, COUTP> ws{WB};
-    conv_layer<P, CINP, COUTP>(X, R0, in_off, pos_lo, pos_hi, ws, epi_of(ws));
+    conv_layer<P, CINP, COUTP>(X, R0, in_off, pos_lo, pos_hi, ws, epi_of(ws), post);
   } else {
     WGlb<P, CINP, COUTP> ws{w};
-    conv_layer<P, CINP, COUTP>(X, R0, in_off, pos_lo, pos_hi, ws, epi_of(ws));
+    conv_layer<P, CINP, COUTP>(X, R0, in_off, pos_lo, pos_hi, ws, epi_of(ws), post);
   }
 }
 
-struct NoStage {
-  __device__ void operator()() const {}
-};
-
-// conv1 + conv2 of a block, in place: positions p in [1, R0-1) then [2, R0-2).
-template <class P, int CINP>
-__device__ __forceinline__ void strip_conv12(char* X, char* WB, int f_start, int F,
-                                             const SepW<typename P::WT, typename P::BT>* w) {
-  constexpr int R0 = strip_slots<P>();
-  strip_layer<P, CINP, kHID>(X, WB, w[0], 0, 1, R0 - 1, [&](auto ws) {
-    return EpiInPlace<P, kHID, decltype(ws)>{X, 0, R0 - 1, f_start, F, ws};
-  }, NoStage{});
-  stamp(2);
-  strip_layer<P, kHID, kHID>(X, WB, w[1], 1, 2, R0 - 2, [&](auto ws) {
-    return EpiInPlace<P, kHID, decltype(ws)>{X, 1, R0 - 2, f_start, F, ws};
-  }, NoStage{});
-}
+static_assert(P16::FO + 4 <= 8 * P16::R, "P16 layers must run in one round (weights are swapped after it)");
 
 // ------------------------------------------------------ dense layers from registers
 // Dense weights: LDS image (P16, staged by the workgroup) or global (P64); K permuted.
@@ -939,23 +951,50 @@ struct EpiConv3 {
   }
 };
 
-// conv3 (positions [3, R0-3)) with the fused epilogue; stages the aggregation MLP with
-// the conv3 weights (P16: W1^T at WB+16K, W2^T at WB+24K, biases in the tail-bias area).
-template <class P, int CHP, int TAILM>
-__device__ __forceinline__ void strip_conv3(const BlockParams<P>& prm, char* X, char* WB, int b, int u,
+// The three layers of a block, in place: conv1 over positions [1, R0-1), conv2 over
+// [2, R0-2), conv3 over [3, R0-3) with the fused epilogue.  P16: conv1's weights are in
+// WB on entry; each layer's global weight loads for the next layer (conv3: + the
+// aggregation MLP) are issued before its math and stored to WB after it.
+template <class P, int CINP, int CHP, int TAILM>
+__device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, char* WB, int b, int u,
                                             int f_start, int mode, typename P::Real wm, bool first) {
   constexpr int R0 = strip_slots<P>();
-  auto extra = [&]() {
+  const int F = prm.a.F;
+  {
+    SepStage<kHID, kHID> nx;
+    if constexpr (P::WLDS) nx.load(prm.w[1]);
+    run_layer<P, CINP, kHID>(X, WB, prm.w[0], 0, 1, R0 - 1, [&](auto ws) {
+      return EpiInPlace<P, kHID, decltype(ws)>{X, 0, R0 - 1, f_start, F, ws};
+    }, [&]() { if constexpr (P::WLDS) nx.store(WB); });
+  }
+  stamp(2);
+  {
+    SepStage<kHID, kDSP> nx;
+    DenseStage<kDSP, kAGG> d1;
+    DenseStage<kAGG, kDSP> d2;
     if constexpr (P::WLDS) {
+      nx.load(prm.w[2]);
       if constexpr (TAILM == TAIL_AGG) {
-        stage_dense<kDSP, kAGG>(WB + 16 * 1024, reinterpret_cast<float*>(WB + kWTailBias), prm.agg[0]);
-        stage_dense<kAGG, kDSP>(WB + 24 * 1024, reinterpret_cast<float*>(WB + kWTailBias + kAGG * 4), prm.agg[1]);
+        d1.load(prm.agg[0]);
+        d2.load(prm.agg[1]);
       }
     }
-  };
-  strip_layer<P, kHID, kDSP>(X, WB, prm.w[2], 2, kHalo, R0 - kHalo, [&](auto ws) {
+    run_layer<P, kHID, kHID>(X, WB, prm.w[1], 1, 2, R0 - 2, [&](auto ws) {
+      return EpiInPlace<P, kHID, decltype(ws)>{X, 1, R0 - 2, f_start, F, ws};
+    }, [&]() {
+      if constexpr (P::WLDS) {
+        nx.store(WB);
+        if constexpr (TAILM == TAIL_AGG) {
+          d1.store(WB + 16 * 1024, reinterpret_cast<float*>(WB + kWTailBias));
+          d2.store(WB + 24 * 1024, reinterpret_cast<float*>(WB + kWTailBias + kAGG * 4));
+        }
+      }
+    });
+  }
+  stamp(3);
+  run_layer<P, kHID, kDSP>(X, WB, prm.w[2], 2, kHalo, R0 - kHalo, [&](auto ws) {
     return EpiConv3<P, decltype(ws), CHP, TAILM>{&prm, X, WB, ws, b, u, f_start, R0 - kHalo, mode, wm, first};
-  }, extra);
+  }, []() {});
 }
 
 // ---------------------------------------------------------------- per-user block bodies
@@ -983,6 +1022,8 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
       *reinterpret_cast<intx4*>(X + xoff<P, NQ>(lf, tt, q)) = intx4{0, 0, 0, 0};
     }
   }
+  SepStage<CINP, kHID> w1;
+  if constexpr (P::WLDS) w1.load(prm.w[0]);
   constexpr int NZ = R0 * kTP * CINP;
   constexpr int BATCH = 32;
   for (int base = 0; base < NZ; base += 512 * BATCH) {
@@ -1017,9 +1058,9 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
       }
     }
   }
+  if constexpr (P::WLDS) w1.store(WB);
   __syncthreads();
-  strip_conv12<P, CINP>(X, WB, f_start, F, prm.w);
-  strip_conv3<P, CHP, TAILM>(prm, X, WB, b, u, f_start, 1, wm, first);
+  strip_block<P, CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 1, wm, first);
 }
 
 // UpdateState of user u on the strip (z = [a, s, pe]).
@@ -1045,6 +1086,8 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
   constexpr int NO = R0 * kTP * (NQ - QS);             // s / pe / pad chunks
   constexpr int PA = (NA + 511) / 512, PO = (NO + 511) / 512;
   const bool inl = prm.inline_combine != 0;
+  SepStage<kUPD_CINP, kHID> w1;
+  if constexpr (P::WLDS) w1.load(prm.w[0]);
   intx4 va[PA][kInlineUsers];
 #pragma unroll
   for (int i = 0; i < PA; ++i) {
@@ -1123,11 +1166,10 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
       *reinterpret_cast<intx4*>(X + xoff<P, NQ>(rowi / kTP, rowi % kTP, q)) = vo[i];
     }
   }
+  if constexpr (P::WLDS) w1.store(WB);
   __syncthreads();
   stamp(1);
-  strip_conv12<P, kUPD_CINP>(X, WB, f_start, F, prm.w);
-  stamp(3);
-  strip_conv3<P, CHP, TAILM>(prm, X, WB, b, u, f_start, 0, 0, false);
+  strip_block<P, kUPD_CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 0, 0, false);
   stamp(4);
 }
 
