@@ -75,6 +75,7 @@ int bits_max(const nrx_desc* d) {
   return b;
 }
 int init_cin(const nrx_desc* d) { return (d->use_h_hat ? 4 : 2) * d->num_rx_ant + 2; }
+int init_a2p(int num_rx_ant) { return 2 * num_rx_ant <= 8 ? 8 : (2 * num_rx_ant <= 16 ? 16 : 32); }
 
 std::vector<LayerShape> layer_list(const nrx_desc* d) {
   std::vector<LayerShape> L;
@@ -143,13 +144,17 @@ struct Packer {
   // offsets relative to blob start, fixed up later
   struct SepOff { size_t dw, pw, b; };
   struct DenOff { size_t w, b; };
-  SepOff sep(const float* dw, const float* pw, const float* b, int cin, int cout, int cinp, int coutp) {
+  // `pos` (optional) places input channel c at packed position pos[c] (StateInit conv1:
+  // the kernel's z image is [y | pe | h] with the antenna blocks padded to A2P).
+  SepOff sep(const float* dw, const float* pw, const float* b, int cin, int cout, int cinp, int coutp,
+             const std::vector<int>* pos = nullptr) {
     std::vector<WT> dwp((size_t)9 * cinp, WT(0)), pwp((size_t)coutp * cinp, WT(0));
     std::vector<BT> bp(coutp, BT(0));
+    auto P = [&](int c) { return pos ? (*pos)[c] : c; };
     for (int tap = 0; tap < 9; ++tap)
-      for (int c = 0; c < cin; ++c) dwp[(size_t)tap * cinp + c] = (WT)dw[(size_t)tap * cin + c];
+      for (int c = 0; c < cin; ++c) dwp[(size_t)tap * cinp + P(c)] = (WT)dw[(size_t)tap * cin + c];
     for (int c = 0; c < cin; ++c)
-      for (int o = 0; o < cout; ++o) pwp[(size_t)o * cinp + c] = (WT)pw[(size_t)c * cout + o];
+      for (int o = 0; o < cout; ++o) pwp[(size_t)o * cinp + P(c)] = (WT)pw[(size_t)c * cout + o];
     for (int o = 0; o < cout; ++o) bp[o] = (BT)b[o];
     SepOff r;
     r.dw = put_w(dwp);
@@ -196,11 +201,20 @@ int build_model(const nrx_desc* d, const float* const* w, int kc, DeviceModel<WT
   DO llr[kMaxHeads][2];
   DO ch[2];
   const int icin = init_cin(d);
-  const int icinp = pow2_at_least(round_up(icin, kc), 32);
+  // StateInit input z = [y (2A), pe (2), h (2A)] (copy_pytorch.py:175-183) is laid out
+  // with each antenna block padded to A2P = init_a2p(A): y at [0, 2A), pe at A2P, A2P+1,
+  // h at [A2P+2, A2P+2+2A); the padded channels carry zero weights.
+  const int a2p = init_a2p(d->num_rx_ant);
+  std::vector<int> ipos(icin);
+  for (int c = 0; c < icin; ++c) {
+    const int a2 = 2 * d->num_rx_ant;
+    ipos[c] = c < a2 ? c : (c < a2 + 2 ? a2p + (c - a2) : a2p + 2 + (c - a2 - 2));
+  }
+  const int icinp = pow2_at_least(round_up(2 * a2p + 2, kc), 32);
   out->init_cinp = icinp;
   int k = 0;
-  auto sep = [&](int cin, int cout, int cinp, int coutp) {
-    SO r = pk.sep(w[k], w[k + 1], w[k + 2], cin, cout, cinp, coutp);
+  auto sep = [&](int cin, int cout, int cinp, int coutp, const std::vector<int>* pos = nullptr) {
+    SO r = pk.sep(w[k], w[k + 1], w[k + 2], cin, cout, cinp, coutp, pos);
     k += 3;
     return r;
   };
@@ -211,7 +225,7 @@ int build_model(const nrx_desc* d, const float* const* w, int kc, DeviceModel<WT
     return r;
   };
   for (int m = 0; m < num_init(d); ++m) {
-    init[m][0] = sep(icin, kHID, icinp, kHID);
+    init[m][0] = sep(icin, kHID, icinp, kHID, &ipos);
     init[m][1] = sep(kHID, kHID, kHID, kHID);
     init[m][2] = sep(kHID, kDS, kHID, kDSP);
   }

@@ -998,12 +998,25 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
 }
 
 // ---------------------------------------------------------------- per-user block bodies
-// StateInit_m of user u on the strip (z = [y*ns, pe, h*ns]).
-template <class P, int CINP, int CHP, int TAILM>
+// StateInit_m of user u on the strip.  z = [y*ns | pe | h*ns] with each antenna block
+// padded to A2P channels (y at [0, 2A), pe at A2P, A2P+1, h at [A2P+2, A2P+2+2A); the host
+// packs conv1's weights to match, nrx_api.cpp build_model).  One thread per (slot, symbol)
+// row of the z image: vector loads of the y / h rows and the pe pair, channel assembly in
+// registers at compile-time positions, then 16-byte LDS stores.
+template <int A2P>
+constexpr int init_cinp(int kc) {
+  int c = (2 * A2P + 2 + kc - 1) / kc * kc;
+  int p = 32;
+  while (p < c) p *= 2;
+  return p;
+}
+
+template <class P, int A2P, int CHP, int TAILM>
 __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem, int b, int u,
                                           int strip, typename P::Real wm, bool first) {
   using S = typename P::S;
   using Real = typename P::Real;
+  constexpr int CINP = init_cinp<A2P>(P::KC);
   constexpr int R0 = strip_slots<P>();
   constexpr int NQZ = CINP * (int)sizeof(S) / 16;
   const auto& a = prm.a;
@@ -1024,37 +1037,44 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
   }
   SepStage<CINP, kHID> w1;
   if constexpr (P::WLDS) w1.load(prm.w[0]);
-  constexpr int NZ = R0 * kTP * CINP;
-  constexpr int BATCH = 32;
-  for (int base = 0; base < NZ; base += 512 * BATCH) {
-    Real v[BATCH];
+  static_assert(R0 * kTP <= 512, "one z row per thread");
+  {
+    const int lf = threadIdx.x / kTP, tt = threadIdx.x % kTP;
+    const int f = f_start + lf;
+    const bool ok = lf < R0 && tt < kT && f >= 0 && f < F;
+    float yv[A2P], hv[A2P];
+    float2 pv = {0.f, 0.f};
+    const size_t re = ((size_t)b * F + (ok ? f : 0)) * kT + (ok ? tt : 0);
+    const float2* yp = reinterpret_cast<const float2*>(a.y + re * A2);
+    const float2* hp = reinterpret_cast<const float2*>(a.h_hat + (((size_t)b * U + u) * F * kT + (re - (size_t)b * F * kT)) * A2);
 #pragma unroll
-    for (int i = 0; i < BATCH; ++i) {
-      const int idx = base + threadIdx.x + i * 512;
-      v[i] = 0;
-      if (idx < NZ) {
-        const int c = idx % CINP;
-        const int tt = (idx / CINP) % kTP;
-        const int lf = idx / (CINP * kTP);
-        const int f = f_start + lf;
-        if (f >= 0 && f < F && tt < kT) {
-          if (c < A2) v[i] = (Real)a.y[(((size_t)b * F + f) * kT + tt) * A2 + c];
-          else if (c < A2 + 2) v[i] = (Real)a.pe[(((size_t)u * F + f) * kT + tt) * 2 + (c - A2)];
-          else if (a.use_h && c < 2 * A2 + 2)
-            v[i] = (Real)a.h_hat[((((size_t)b * U + u) * F + f) * kT + tt) * A2 + (c - A2 - 2)];
-        }
+    for (int k = 0; k < A2P / 2; ++k) {
+      float2 v = {0.f, 0.f}, w = {0.f, 0.f};
+      if (ok && 2 * k < A2) {
+        v = yp[k];
+        if (a.use_h) w = hp[k];
       }
+      yv[2 * k] = v.x;
+      yv[2 * k + 1] = v.y;
+      hv[2 * k] = w.x;
+      hv[2 * k + 1] = w.y;
     }
+    if (ok) pv = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + f) * kT + tt) * 2);
+    if (lf < R0) {
 #pragma unroll
-    for (int i = 0; i < BATCH; ++i) {
-      const int idx = base + threadIdx.x + i * 512;
-      if (idx < NZ) {
-        const int c = idx % CINP;
-        const int tt = (idx / CINP) % kTP;
-        const int lf = idx / (CINP * kTP);
-        const Real sc = (c < A2 || (c >= A2 + 2 && c < 2 * A2 + 2)) ? ns : (Real)1;
-        *reinterpret_cast<S*>(X + xoff<P, NQZ>(lf, tt, c / P::EPC) + (c % P::EPC) * (int)sizeof(S)) =
-            (S)(v[i] * sc);
+      for (int q = 0; q < NQZ; ++q) {
+        S o[P::EPC];
+#pragma unroll
+        for (int e = 0; e < P::EPC; ++e) {
+          const int c = q * P::EPC + e;
+          Real v = 0;
+          if (c < A2P) v = (Real)yv[c] * ns;
+          else if (c == A2P) v = (Real)pv.x;
+          else if (c == A2P + 1) v = (Real)pv.y;
+          else if (c < 2 * A2P + 2) v = (Real)hv[c - A2P - 2] * ns;
+          o[e] = (S)v;
+        }
+        *reinterpret_cast<intx4*>(X + xoff<P, NQZ>(lf, tt, q)) = *reinterpret_cast<const intx4*>(o);
       }
     }
   }
@@ -1079,49 +1099,71 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
   // z chunks: [0,QS) <- a, [QS,2QS) <- s, 2QS <- pe (2 values), rest 0.
   // a_u = (sum_u' sp_u' - sp_u) * p is formed here from the producer's act*sp rows when
   // U <= kInlineUsers (AggregateUserStates' leave-one-out mean, neural_rx.py:191-204);
-  // otherwise k_combine already wrote a_u in place.  All global loads of a thread are
-  // issued first, then the LDS stores.
+  // otherwise k_combine already wrote a_u in place.
+  // The in-grid rows [lo, hi) of a (b, u) plane are one contiguous range of the compact
+  // [F][14][56] layout, so chunk c of it is simply base + 16 c: all global loads are
+  // issued first (32-bit offsets from a wave-uniform base), then the LDS stores.
   using Real = typename P::Real;
-  constexpr int NA = R0 * kTP * QS;                    // a chunks
-  constexpr int NO = R0 * kTP * (NQ - QS);             // s / pe / pad chunks
-  constexpr int PA = (NA + 511) / 512, PO = (NO + 511) / 512;
+  constexpr int NV_MAX = R0 * kT * QS;
+  constexpr int PV = (NV_MAX + 511) / 512;
+  const int lo = f_start < 0 ? 0 : f_start;
+  const int hi = f_start + R0 < F ? f_start + R0 : F;
+  const int slot_lo = lo - f_start, nrow = hi - lo;
+  const unsigned NV = (unsigned)(nrow * kT * QS);
   const bool inl = prm.inline_combine != 0;
+  // planes read for a: inline -> the U-1 other users' act*sp rows; else the combined a_u
+  const int no = inl ? U - 1 : 1;
   SepStage<kUPD_CINP, kHID> w1;
   if constexpr (P::WLDS) w1.load(prm.w[0]);
-  intx4 va[PA][kInlineUsers];
+  const intx4* sb = reinterpret_cast<const intx4*>(a.s_in + srow(b, u, lo, 0, U, F));
+  const intx4* ab[kInlineUsers - 1];
 #pragma unroll
-  for (int i = 0; i < PA; ++i) {
-    const int idx = threadIdx.x + i * 512;
-    const int rowi = idx / QS, q = idx % QS;
-    const int tt = rowi % kTP, lf = rowi / kTP;
-    const int f = f_start + lf;
-    const bool ok = !(NRX_ABLATE & 2) && idx < NA && f >= 0 && f < F && tt < kT;
-#pragma unroll
-    for (int uu = 0; uu < kInlineUsers; ++uu) {
-      va[i][uu] = intx4{0, 0, 0, 0};
-      if (ok && uu < (inl ? U : 1))
-        va[i][uu] = *reinterpret_cast<const intx4*>(a.a + srow(b, inl ? uu : u, f, tt, U, F) + q * P::EPC);
-    }
+  for (int k = 0; k < kInlineUsers - 1; ++k) {
+    const int uu = inl ? (k < u ? k : k + 1) : u;
+    ab[k] = reinterpret_cast<const intx4*>(a.a + srow(b, uu < U ? uu : 0, lo, 0, U, F));
   }
-  intx4 vo[PO];
+  intx4 vs[PV], va[PV][kInlineUsers - 1];
 #pragma unroll
-  for (int i = 0; i < PO; ++i) {
-    const int idx = threadIdx.x + i * 512;
-    const int rowi = idx / (NQ - QS), q = QS + idx % (NQ - QS);
-    const int tt = rowi % kTP, lf = rowi / kTP;
-    const int f = f_start + lf;
-    vo[i] = intx4{0, 0, 0, 0};
-    if (!(NRX_ABLATE & 2) && idx < NO && f >= 0 && f < F && tt < kT) {
-      const size_t row = srow(b, u, f, tt, U, F);
-      if (q < 2 * QS) {
-        vo[i] = *reinterpret_cast<const intx4*>(a.s_in + row + (q - QS) * P::EPC);
-      } else if (q == 2 * QS) {
-        const float* pp = a.pe + (((size_t)u * F + f) * kT + tt) * 2;
-        S pe2[P::EPC] = {};
-        pe2[0] = (S)pp[0];
-        pe2[1] = (S)pp[1];
-        vo[i] = *reinterpret_cast<const intx4*>(pe2);
+  for (int i = 0; i < PV; ++i) {
+    unsigned c = threadIdx.x + 512u * i;
+    if (NRX_ABLATE & 2) c = 0;
+    c = c < NV ? c : 0;          // tail lanes re-read chunk 0 and store nothing
+    vs[i] = sb[c];
+#pragma unroll
+    for (int k = 0; k < kInlineUsers - 1; ++k) va[i][k] = k < no ? ab[k][c] : intx4{0, 0, 0, 0};
+  }
+  // fixed chunks while the loads fly: t = 14, 15 (all chunks) and, for t < 14, the pe chunk
+  // (2QS) and the zero pad chunks (2QS, NQ)
+  {
+    constexpr int NX = NQ - 2 * QS;                  // pe + pad chunks per symbol
+    constexpr int PER_SLOT = 2 * NQ + kT * NX;
+    for (int idx = threadIdx.x; idx < R0 * PER_SLOT; idx += 512) {
+      const int slot = idx / PER_SLOT, k = idx % PER_SLOT;
+      int tt, q;
+      if (k < 2 * NQ) {
+        tt = kT + k / NQ;
+        q = k % NQ;
+      } else {
+        tt = (k - 2 * NQ) / NX;
+        q = 2 * QS + (k - 2 * NQ) % NX;
       }
+      intx4 v = intx4{0, 0, 0, 0};
+      const int f = f_start + slot;
+      if (q == 2 * QS && tt < kT && f >= 0 && f < F) {
+        const float2 pp = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + f) * kT + tt) * 2);
+        S pe2[P::EPC] = {};
+        pe2[0] = (S)pp.x;
+        pe2[1] = (S)pp.y;
+        v = *reinterpret_cast<const intx4*>(pe2);
+      }
+      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(slot, tt, q)) = v;
+    }
+    // a / s chunks of the slots outside the grid (edge strips only)
+    const int nout = R0 - nrow;
+    for (int idx = threadIdx.x; idx < nout * kT * 2 * QS; idx += 512) {
+      const int j = idx / (kT * 2 * QS), k = idx % (kT * 2 * QS);
+      const int slot = j < slot_lo ? j : nrow + j;
+      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(slot, k / (2 * QS), k % (2 * QS))) = intx4{0, 0, 0, 0};
     }
   }
   Real pf = 1;
@@ -1132,38 +1174,37 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
     pf = pf > (Real)0 ? (Real)1 / pf : (Real)1;
   }
 #pragma unroll
-  for (int i = 0; i < PA; ++i) {
-    const int idx = threadIdx.x + i * 512;
-    if (idx < NA) {
-      const int rowi = idx / QS, q = idx % QS;
+  for (int i = 0; i < PV; ++i) {
+    const unsigned c = threadIdx.x + 512u * i;
+    if (c < NV) {
+      const int pair = c / QS, q = c % QS;
+      const int slot = slot_lo + pair / kT, tt = pair % kT;
       intx4 out = va[i][0];
       if (inl) {
-        Real sum[P::EPC], own[P::EPC];
+        // a_u = p * sum of the other users' act*sp (packed f16 adds in the f16 policy; one
+        // plane with p = 1, e.g. U = 2 with a 0/1 mask, stays exact)
+        if constexpr (sizeof(S) == 2) {
+          half8 sm = __builtin_bit_cast(half8, va[i][0]);
 #pragma unroll
-        for (int e = 0; e < P::EPC; ++e) sum[e] = own[e] = 0;
-#pragma unroll
-        for (int uu = 0; uu < kInlineUsers; ++uu) {
-          const S* sv = reinterpret_cast<const S*>(&va[i][uu]);
+          for (int k = 1; k < kInlineUsers - 1; ++k)
+            if (k < no) sm += __builtin_bit_cast(half8, va[i][k]);
+          if (pf != (Real)1) sm *= (_Float16)pf;
+          out = no > 0 ? __builtin_bit_cast(intx4, sm) : intx4{0, 0, 0, 0};
+        } else {
+          S o[P::EPC];
 #pragma unroll
           for (int e = 0; e < P::EPC; ++e) {
-            sum[e] += (Real)sv[e];
-            if (uu == u) own[e] = (Real)sv[e];
+            Real sum = 0;
+#pragma unroll
+            for (int k = 0; k < kInlineUsers - 1; ++k)
+              if (k < no) sum += (Real)reinterpret_cast<const S*>(&va[i][k])[e];
+            o[e] = (S)(sum * pf);
           }
+          out = *reinterpret_cast<const intx4*>(o);
         }
-        S o[P::EPC];
-#pragma unroll
-        for (int e = 0; e < P::EPC; ++e) o[e] = (S)((sum[e] - own[e]) * pf);
-        out = *reinterpret_cast<const intx4*>(o);
       }
-      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(rowi / kTP, rowi % kTP, q)) = out;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < PO; ++i) {
-    const int idx = threadIdx.x + i * 512;
-    if (idx < NO) {
-      const int rowi = idx / (NQ - QS), q = QS + idx % (NQ - QS);
-      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(rowi / kTP, rowi % kTP, q)) = vo[i];
+      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(slot, tt, q)) = out;
+      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(slot, tt, QS + q)) = vs[i];
     }
   }
   if constexpr (P::WLDS) w1.store(WB);
@@ -1215,7 +1256,7 @@ __global__ __launch_bounds__(256) void k_combine(typename P::S* __restrict__ buf
 // StateInit_m (+ Var-IO mix: one launch per m, m > 0 accumulating) of one (slot, user,
 // strip); the last launch applies the aggregation MLP of iteration 0 (stores act * sp).
 // grid = (strips, U, B).
-template <class P, int CINP, int CHP, int TAILM>
+template <class P, int A2P, int TAILM>
 __global__ __launch_bounds__(512) void k_init(BlockParams<P> prm) {
   using Real = typename P::Real;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1228,7 +1269,7 @@ __global__ __launch_bounds__(512) void k_init(BlockParams<P> prm) {
     wm = a.mcs_mask ? (Real)a.mcs_mask[((size_t)b * U + u) * a.M + m] : (Real)(m == 0 ? 1 : 0);
   // wm == 0: this MCS contributes exactly 0 * finite; the conv math is still run (the
   // m = 0 launch defines s, the last launch applies the aggregation MLP).
-  init_user<P, CINP, CHP, TAILM>(prm, smem, b, u, strip, wm, m == 0);
+  init_user<P, A2P, 16, TAILM>(prm, smem, b, u, strip, wm, m == 0);
 }
 
 // UpdateState of one (slot, user, strip) with the fused tail.  grid = (strips, U, B).
@@ -1253,11 +1294,10 @@ struct Launch {
       hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, strip_lds_bytes<P>());
       if (r != hipSuccess) e = r;
     };
-#define NRX_SET_INIT(C, CH)                                   \
-    set((const void*)k_init<P, C, CH, TAIL_NONE>);            \
-    set((const void*)k_init<P, C, CH, TAIL_AGG>);
-    NRX_SET_INIT(32, 16) NRX_SET_INIT(64, 16) NRX_SET_INIT(128, 16)
-    NRX_SET_INIT(32, 32) NRX_SET_INIT(64, 32) NRX_SET_INIT(128, 32)
+#define NRX_SET_INIT(A2P)                                     \
+    set((const void*)k_init<P, A2P, TAIL_NONE>);              \
+    set((const void*)k_init<P, A2P, TAIL_AGG>);
+    NRX_SET_INIT(8) NRX_SET_INIT(16) NRX_SET_INIT(32)
 #undef NRX_SET_INIT
     set((const void*)k_update<P, 16, TAIL_AGG>);
     set((const void*)k_update<P, 16, TAIL_READOUT>);
@@ -1266,10 +1306,11 @@ struct Launch {
     return e;
   }
 
-  template <int C, int CH>
+  template <int A2P>
   static void launch_init(dim3 grid, int L, hipStream_t st, const BlockParams<P>& bp, bool tail) {
-    if (tail) k_init<P, C, CH, TAIL_AGG><<<grid, 512, L, st>>>(bp);
-    else k_init<P, C, CH, TAIL_NONE><<<grid, 512, L, st>>>(bp);
+    static_assert(init_cinp<A2P>(P::KC) <= kHID, "StateInit input wider than the strip image");
+    if (tail) k_init<P, A2P, TAIL_AGG><<<grid, 512, L, st>>>(bp);
+    else k_init<P, A2P, TAIL_NONE><<<grid, 512, L, st>>>(bp);
   }
 
   static hipError_t run(const A& args0, const MW& W, int num_it, hipStream_t st, Prof* prof) {
@@ -1307,9 +1348,10 @@ struct Launch {
       bp.agg[0] = W.agg[0][0];
       bp.agg[1] = W.agg[0][1];
       const bool tl = bp.tail == TAIL_AGG;
-      if (args.init_cinp <= 32) ch32 ? launch_init<32, 32>(grid, L, st, bp, tl) : launch_init<32, 16>(grid, L, st, bp, tl);
-      else if (args.init_cinp <= 64) ch32 ? launch_init<64, 32>(grid, L, st, bp, tl) : launch_init<64, 16>(grid, L, st, bp, tl);
-      else ch32 ? launch_init<128, 32>(grid, L, st, bp, tl) : launch_init<128, 16>(grid, L, st, bp, tl);
+      // antenna block padding A2P (must match nrx_api.cpp init_a2p)
+      if (2 * args.A <= 8) launch_init<8>(grid, L, st, bp, tl);
+      else if (2 * args.A <= 16) launch_init<16>(grid, L, st, bp, tl);
+      else launch_init<32>(grid, L, st, bp, tl);
     }
     E_(K_INIT);
     combine(bp.a.a_out);
