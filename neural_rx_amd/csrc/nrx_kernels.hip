@@ -47,7 +47,7 @@ namespace nrx {
 
 #ifdef NRX_STAMPS
 // diagnostic builds only: s_memtime per phase, wave 0 lane 0 of each workgroup
-__device__ unsigned long long g_nrx_stamps[4096][8];
+__device__ unsigned long long g_nrx_stamps[4096][32];
 __device__ int g_nrx_stamp_on;   // set by the host for the k_update launch to record
 __device__ __forceinline__ void stamp(int k) {
   if (threadIdx.x == 0 && g_nrx_stamp_on) {
@@ -411,6 +411,7 @@ __device__ __forceinline__ void conv_layer(const char* X, int nslots, int in_off
     const bool act = p0 < pos_hi;
     typename P::Acc acc[P::R][COUTP / 16];
     typename std::decay_t<Epi>::Pref pf;
+    stamp(8 + 5 * in_off);
     if (act) epi.prefetch(pf, p0, t, g);     // epilogue global loads, in flight during the math
     if (act) {
       if constexpr (NRX_ABLATE & 1) {
@@ -422,10 +423,14 @@ __device__ __forceinline__ void conv_layer(const char* X, int nslots, int in_off
         conv_rows<P, CINP, COUTP>(X, p0 - in_off, nslots, t, g, lane, ws, acc);
       }
     }
+    stamp(9 + 5 * in_off);
     __syncthreads();
+    stamp(10 + 5 * in_off);
     if (base == pos_lo) post_math();   // all threads: this layer's weights are dead (P16)
     epi.pre();                       // all threads (e.g. stage tail weights into X)
+    stamp(11 + 5 * in_off);
     if (act) epi(acc, pf, p0, t, g);
+    stamp(12 + 5 * in_off);
     __syncthreads();
   }
 }
@@ -756,14 +761,12 @@ struct EpiConv3 {
   __device__ void pre() const {
     if constexpr (P::WLDS) {
       if constexpr (TAILM == TAIL_READOUT) {
-        // stage the readout heads into X (every wave is past its conv3 reads)
+        // LLR head 0 and the ChEst head were prefetched during the conv3 math and stored
+        // into X by strip_block; stage any further heads (Var-IO) now
         const auto& a = prm->a;
-        for (int h = 0; h <= a.H; ++h) {
-          const bool ch = h == a.H;
-          const DenseW<_Float16, float>* d = ch ? prm->chest : prm->llr[h];
-          stage_dense<kDSP, kHID>(X + head_w1(h), reinterpret_cast<float*>(X + head_b1(h)), d[0]);
-          if (ch) stage_dense<kHID, CHP>(X + head_w2(h), reinterpret_cast<float*>(X + head_b2(h)), d[1]);
-          else stage_dense<kHID, 16>(X + head_w2(h), reinterpret_cast<float*>(X + head_b2(h)), d[1]);
+        for (int h = 1; h < a.H; ++h) {
+          stage_dense<kDSP, kHID>(X + head_w1(h), reinterpret_cast<float*>(X + head_b1(h)), prm->llr[h][0]);
+          stage_dense<kHID, 16>(X + head_w2(h), reinterpret_cast<float*>(X + head_b2(h)), prm->llr[h][1]);
         }
         __syncthreads();
       }
@@ -802,6 +805,7 @@ struct EpiConv3 {
   }
 
   __device__ void operator()(const typename P::Acc (&acc)[R][NTS], const Pref& pf, int p0, int t, int g) const {
+    stamp(6);
     const auto& a = prm->a;
     const int F = a.F, U = a.U;
     const int lane = threadIdx.x & 63;
@@ -951,6 +955,13 @@ struct EpiConv3 {
   }
 };
 
+// Register prefetch of the next layer's weights during the current layer's math (off: they
+// are fetched after it, latency exposed, registers free for the conv pipeline).
+#ifndef NRX_PREFETCH_W
+#define NRX_PREFETCH_W 1
+#endif
+constexpr bool kPrefetchW = NRX_PREFETCH_W != 0;
+
 // The three layers of a block, in place: conv1 over positions [1, R0-1), conv2 over
 // [2, R0-2), conv3 over [3, R0-3) with the fused epilogue.  P16: conv1's weights are in
 // WB on entry; each layer's global weight loads for the next layer (conv3: + the
@@ -962,27 +973,36 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
   const int F = prm.a.F;
   {
     SepStage<kHID, kHID> nx;
-    if constexpr (P::WLDS) nx.load(prm.w[1]);
+    if constexpr (P::WLDS && kPrefetchW) nx.load(prm.w[1]);
     run_layer<P, CINP, kHID>(X, WB, prm.w[0], 0, 1, R0 - 1, [&](auto ws) {
       return EpiInPlace<P, kHID, decltype(ws)>{X, 0, R0 - 1, f_start, F, ws};
-    }, [&]() { if constexpr (P::WLDS) nx.store(WB); });
+    }, [&]() {
+      if constexpr (P::WLDS) {
+        if constexpr (!kPrefetchW) nx.load(prm.w[1]);
+        nx.store(WB);
+      }
+    });
   }
   stamp(2);
   {
     SepStage<kHID, kDSP> nx;
     DenseStage<kDSP, kAGG> d1;
     DenseStage<kAGG, kDSP> d2;
-    if constexpr (P::WLDS) {
-      nx.load(prm.w[2]);
-      if constexpr (TAILM == TAIL_AGG) {
-        d1.load(prm.agg[0]);
-        d2.load(prm.agg[1]);
+    auto ld = [&]() {
+      if constexpr (P::WLDS) {
+        nx.load(prm.w[2]);
+        if constexpr (TAILM == TAIL_AGG) {
+          d1.load(prm.agg[0]);
+          d2.load(prm.agg[1]);
+        }
       }
-    }
+    };
+    if constexpr (P::WLDS && kPrefetchW) ld();
     run_layer<P, kHID, kHID>(X, WB, prm.w[1], 1, 2, R0 - 2, [&](auto ws) {
       return EpiInPlace<P, kHID, decltype(ws)>{X, 1, R0 - 2, f_start, F, ws};
     }, [&]() {
       if constexpr (P::WLDS) {
+        if constexpr (!kPrefetchW) ld();
         nx.store(WB);
         if constexpr (TAILM == TAIL_AGG) {
           d1.store(WB + 16 * 1024, reinterpret_cast<float*>(WB + kWTailBias));
@@ -992,9 +1012,34 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
     });
   }
   stamp(3);
-  run_layer<P, kHID, kDSP>(X, WB, prm.w[2], 2, kHalo, R0 - kHalo, [&](auto ws) {
-    return EpiConv3<P, decltype(ws), CHP, TAILM>{&prm, X, WB, ws, b, u, f_start, R0 - kHalo, mode, wm, first};
-  }, []() {});
+  {
+    // readout tail: LLR head 0 and ChEst weights are fetched during the conv3 math and
+    // stored into the strip image X once every wave is past its conv3 reads
+    DenseStage<kDSP, kHID> l1, c1;
+    DenseStage<kHID, 16> l2;
+    DenseStage<kHID, CHP> c2;
+    auto ld = [&]() {
+      if constexpr (P::WLDS) {
+        l1.load(prm.llr[0][0]);
+        l2.load(prm.llr[0][1]);
+        c1.load(prm.chest[0]);
+        c2.load(prm.chest[1]);
+      }
+    };
+    if constexpr (P::WLDS && TAILM == TAIL_READOUT && kPrefetchW) ld();
+    run_layer<P, kHID, kDSP>(X, WB, prm.w[2], 2, kHalo, R0 - kHalo, [&](auto ws) {
+      return EpiConv3<P, decltype(ws), CHP, TAILM>{&prm, X, WB, ws, b, u, f_start, R0 - kHalo, mode, wm, first};
+    }, [&]() {
+      if constexpr (P::WLDS && TAILM == TAIL_READOUT) {
+        if constexpr (!kPrefetchW) ld();
+        const int H = prm.a.H;
+        l1.store(X + head_w1(0), reinterpret_cast<float*>(X + head_b1(0)));
+        l2.store(X + head_w2(0), reinterpret_cast<float*>(X + head_b2(0)));
+        c1.store(X + head_w1(H), reinterpret_cast<float*>(X + head_b1(H)));
+        c2.store(X + head_w2(H), reinterpret_cast<float*>(X + head_b2(H)));
+      }
+    });
+  }
 }
 
 // ---------------------------------------------------------------- per-user block bodies
@@ -1132,8 +1177,15 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
 #pragma unroll
     for (int k = 0; k < kInlineUsers - 1; ++k) va[i][k] = k < no ? ab[k][c] : intx4{0, 0, 0, 0};
   }
-  // fixed chunks while the loads fly: t = 14, 15 (all chunks) and, for t < 14, the pe chunk
-  // (2QS) and the zero pad chunks (2QS, NQ)
+  // pe chunk (2 values) of z row (slot, t < 14): one row per thread, loaded with the rest
+  static_assert(R0 * kT <= 512, "one pe row per thread");
+  const int pe_slot = threadIdx.x / kT, pe_t = threadIdx.x % kT;
+  const int pe_f = f_start + pe_slot;
+  const bool pe_ok = pe_slot < R0 && pe_f >= 0 && pe_f < F;
+  float2 pe_v = {0.f, 0.f};
+  if (pe_ok) pe_v = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + pe_f) * kT + pe_t) * 2);
+  // fixed zero chunks while the loads fly: t = 14, 15 (all chunks) and, for t < 14, the
+  // pad chunks (2QS, NQ) (the pe chunk 2QS is overwritten below)
   {
     constexpr int NX = NQ - 2 * QS;                  // pe + pad chunks per symbol
     constexpr int PER_SLOT = 2 * NQ + kT * NX;
@@ -1147,16 +1199,7 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
         tt = (k - 2 * NQ) / NX;
         q = 2 * QS + (k - 2 * NQ) % NX;
       }
-      intx4 v = intx4{0, 0, 0, 0};
-      const int f = f_start + slot;
-      if (q == 2 * QS && tt < kT && f >= 0 && f < F) {
-        const float2 pp = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + f) * kT + tt) * 2);
-        S pe2[P::EPC] = {};
-        pe2[0] = (S)pp.x;
-        pe2[1] = (S)pp.y;
-        v = *reinterpret_cast<const intx4*>(pe2);
-      }
-      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(slot, tt, q)) = v;
+      if (q != 2 * QS || tt >= kT) *reinterpret_cast<intx4*>(X + xoff<P, NQ>(slot, tt, q)) = intx4{0, 0, 0, 0};
     }
     // a / s chunks of the slots outside the grid (edge strips only)
     const int nout = R0 - nrow;
@@ -1165,6 +1208,12 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
       const int slot = j < slot_lo ? j : nrow + j;
       *reinterpret_cast<intx4*>(X + xoff<P, NQ>(slot, k / (2 * QS), k % (2 * QS))) = intx4{0, 0, 0, 0};
     }
+  }
+  if (pe_slot < R0) {
+    S pe2[P::EPC] = {};
+    pe2[0] = (S)pe_v.x;
+    pe2[1] = (S)pe_v.y;
+    *reinterpret_cast<intx4*>(X + xoff<P, NQ>(pe_slot, pe_t, 2 * QS)) = *reinterpret_cast<const intx4*>(pe2);
   }
   Real pf = 1;
   if (inl) {
@@ -1410,7 +1459,7 @@ int strip_width(int precision) { return precision == 0 ? P16::FO : P64::FO; }
 
 #ifdef NRX_STAMPS
 extern "C" int nrx_debug_stamps(void* out, int n) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nrx_stamps), (size_t)n * 8 * 8, 0, hipMemcpyDeviceToHost);
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nrx_stamps), (size_t)n * 32 * 8, 0, hipMemcpyDeviceToHost);
 }
 #endif
 

@@ -22,13 +22,21 @@ for _ in range(5):
     eng.forward(t(sl.y), pe, t(sl.h_hat), t(sl.active), None, 2, "f16")
 torch.cuda.synchronize()
 n = 512
-buf = np.zeros((n, 8), np.uint64)
+buf = np.zeros((n, 32), np.uint64)
 lib.nrx_debug_stamps(buf.ctypes.data, n)
-st = buf[:, :6].astype(np.int64)
+st = buf[:, [0, 1, 2, 3, 6, 4, 5]].astype(np.int64)
 d = np.diff(st, axis=1)
-names = ["z-load", "conv1", "conv2", "conv3+epi", "tail"]
+names = ["z-load", "conv1", "conv2", "conv3", "epilogue", "tail"]
+launch = os.environ.get("NRX_STAMP_LAUNCH", "0")
 print("k_update launch", os.environ.get("NRX_STAMP_LAUNCH", "0"))
-tot = st[:, 5] - st[:, 0]
+tot = st[:, -1] - st[:, 0]
 print("cycles per WG (mean):", tot.mean(), " start spread:", st[:, 0].max() - st[:, 0].min())
 for i, nm in enumerate(names):
     print(f"  {nm:10s} mean {d[:, i].mean():9.0f}  ({100 * d[:, i].mean() / tot.mean():5.1f}%)  max {d[:, i].max()}")
+
+# conv_layer detail (wave 0): math | barrier1 | post+pre | epilogue (own rows)
+det = buf[:, 8:23].astype(np.int64).reshape(n, 3, 5)
+for L in range(3):
+    seg = np.diff(det[:, L, :], axis=1)
+    print(f"  conv{L + 1}: math {seg[:, 0].mean():7.0f}  bar1 {seg[:, 1].mean():7.0f}  "
+          f"post {seg[:, 2].mean():7.0f}  epi {seg[:, 3].mean():7.0f}")
