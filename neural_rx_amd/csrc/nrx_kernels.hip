@@ -48,10 +48,12 @@ namespace nrx {
 #ifdef NRX_STAMPS
 // diagnostic builds only: s_memtime per phase, wave 0 lane 0 of each workgroup
 __device__ unsigned long long g_nrx_stamps[4096][32];
-__device__ int g_nrx_stamp_on;   // set by the host for the k_update launch to record
+// set by the host for the k_update launch to record; __constant__ so that the flag is a
+// scalar (SMEM) load and a stamp does not wait for the wave's outstanding vector loads
+__constant__ int g_nrx_stamp_on;
 __device__ __forceinline__ void stamp(int k) {
   if (threadIdx.x == 0 && g_nrx_stamp_on) {
-    const int wg = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const int wg = blockIdx.x;
     if (wg < 4096) g_nrx_stamps[wg][k] = __builtin_amdgcn_s_memtime();
   }
 }
@@ -424,14 +426,25 @@ __device__ __forceinline__ void conv_layer(const char* X, int nslots, int in_off
       }
     }
     stamp(9 + 5 * in_off);
-    __syncthreads();
-    stamp(10 + 5 * in_off);
-    if (base == pos_lo) post_math();   // all threads: this layer's weights are dead (P16)
-    epi.pre();                       // all threads (e.g. stage tail weights into X)
-    stamp(11 + 5 * in_off);
-    if (act) epi(acc, pf, p0, t, g);
-    stamp(12 + 5 * in_off);
-    __syncthreads();
+    using E = std::decay_t<Epi>;
+    if constexpr (E::kNoBarrier) {
+      // the epilogue neither writes LDS nor reads anything staged after the math: each
+      // wave runs it as soon as its own math is done (post_math is empty for these)
+      if (act) epi(acc, pf, p0, t, g, 0, P::R);
+      stamp(12 + 5 * in_off);
+    } else {
+      // rows r >= kEarlyRow of an in-place layer land in slots no other wave reads this
+      // round (wave w-1 reads up to slot p0 - in_off): written before the barrier
+      if (act) epi(acc, pf, p0, t, g, E::kEarlyRow, P::R);
+      __syncthreads();
+      stamp(10 + 5 * in_off);
+      if (base == pos_lo) post_math();   // all threads: this layer's weights are dead (P16)
+      epi.pre();                       // all threads (e.g. stage tail weights into X)
+      stamp(11 + 5 * in_off);
+      if (act) epi(acc, pf, p0, t, g, 0, E::kEarlyRow);
+      stamp(12 + 5 * in_off);
+      __syncthreads();
+    }
   }
 }
 
@@ -443,18 +456,21 @@ struct NoPref {};
 template <class P, int COUTP, class WS>
 struct EpiInPlace {
   using Pref = NoPref;
+  static constexpr bool kNoBarrier = false;
+  static constexpr int kEarlyRow = 2 < P::R ? 2 : P::R;
   char* X;
   int in_off, pos_hi, f_start, F;
   WS ws;
   __device__ void pre() const {}
   __device__ void prefetch(Pref&, int, int, int) const {}
   __device__ void operator()(const typename P::Acc (&acc)[P::R][COUTP / 16], const Pref&, int p0, int t,
-                             int g) const {
+                             int g, int r_lo, int r_hi) const {
     using Real = typename P::Real;
     using S = typename P::S;
     constexpr int NQ = COUTP * (int)sizeof(S) / 16;
 #pragma unroll
     for (int r = 0; r < P::R; ++r) {
+      if (r < r_lo || r >= r_hi) continue;
       const int p = p0 + r;
       if (p >= pos_hi) continue;
       const int f = f_start + p;
@@ -585,6 +601,8 @@ struct BlockParams {
   DenseW<typename P::WT, typename P::BT> chest[2];
   int tail;                                              // TAIL_AGG / TAIL_READOUT / TAIL_NONE
   int m;                                                 // init: which StateInit (Var-IO)
+  int strips;                                            // strips per (slot, user)
+  int order_rev;                                         // XCD-local work order reversed
   int inline_combine;                                    // U <= kInlineUsers: z-load forms a
 };
 
@@ -722,6 +740,9 @@ struct EpiConv3 {
   struct Pref {
     std::conditional_t<sizeof(S) == 2, half4, Real[4]> prev[R][NTS];
   };
+  // no LDS writes; the readout tail reads head weights staged into X after the math
+  static constexpr bool kNoBarrier = TAILM != TAIL_READOUT;
+  static constexpr int kEarlyRow = P::R;   // readout: every row after the barrier
   const BlockParams<P>* prm;
   char* X;
   char* WB;
@@ -804,7 +825,9 @@ struct EpiConv3 {
     dense_rows<P, kHID / 16, NO * 16, RB>(hb, w2, lane, g, o, false);
   }
 
-  __device__ void operator()(const typename P::Acc (&acc)[R][NTS], const Pref& pf, int p0, int t, int g) const {
+  __device__ void operator()(const typename P::Acc (&acc)[R][NTS], const Pref& pf, int p0, int t, int g,
+                             int r_lo, int r_hi) const {
+    if (r_lo >= r_hi) return;        // all R rows in one call
     stamp(6);
     const auto& a = prm->a;
     const int F = a.F, U = a.U;
@@ -1182,8 +1205,11 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
   const int pe_slot = threadIdx.x / kT, pe_t = threadIdx.x % kT;
   const int pe_f = f_start + pe_slot;
   const bool pe_ok = pe_slot < R0 && pe_f >= 0 && pe_f < F;
-  float2 pe_v = {0.f, 0.f};
-  if (pe_ok) pe_v = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + pe_f) * kT + pe_t) * 2);
+  // unconditional load from a clamped address (no branch around it: a conditional load
+  // makes the compiler convert right after it, i.e. wait for every load issued above)
+  const float2 pe_v = *reinterpret_cast<const float2*>(
+      a.pe + (((size_t)u * F + (pe_ok ? pe_f : 0)) * kT + (pe_ok ? pe_t : 0)) * 2);
+  stamp(24);
   // fixed zero chunks while the loads fly: t = 14, 15 (all chunks) and, for t < 14, the
   // pad chunks (2QS, NQ) (the pe chunk 2QS is overwritten below)
   {
@@ -1209,10 +1235,11 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
       *reinterpret_cast<intx4*>(X + xoff<P, NQ>(slot, k / (2 * QS), k % (2 * QS))) = intx4{0, 0, 0, 0};
     }
   }
+  stamp(25);
   if (pe_slot < R0) {
     S pe2[P::EPC] = {};
-    pe2[0] = (S)pe_v.x;
-    pe2[1] = (S)pe_v.y;
+    pe2[0] = pe_ok ? (S)pe_v.x : (S)0;
+    pe2[1] = pe_ok ? (S)pe_v.y : (S)0;
     *reinterpret_cast<intx4*>(X + xoff<P, NQ>(pe_slot, pe_t, 2 * QS)) = *reinterpret_cast<const intx4*>(pe2);
   }
   Real pf = 1;
@@ -1256,11 +1283,39 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
       *reinterpret_cast<intx4*>(X + xoff<P, NQ>(slot, tt, QS + q)) = vs[i];
     }
   }
+  stamp(26);
   if constexpr (P::WLDS) w1.store(WB);
+  stamp(27);
   __syncthreads();
   stamp(1);
   strip_block<P, kUPD_CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 0, 0, false);
   stamp(4);
+}
+
+// ------------------------------------------------------------ work-item placement
+// 1-D grid of B * U * strips workgroups.  Workgroups are dispatched to the 8 XCDs round-
+// robin by linear id (cdna_hip_programming.md T1: id % 8 labels the XCD), so the items of
+// one slot -- which exchange users' aggregates and strip halos through HBM between
+// launches -- are given ids with one residue mod 8: everything a workgroup reads was
+// written on its own XCD, through its L2.  Consecutive launches alternate the order within
+// an XCD (order_rev) so that the items written last, the most likely still in L2, are
+// read first.  Slots beyond the last complete group of 8 keep the plain order.
+__device__ __forceinline__ void work_item(int i, int B, int U, int S, int rev, int& b, int& u, int& strip) {
+  const int ips = U * S;
+  const int per_xcd = (B / 8) * ips;
+  int k;
+  if (i < 8 * per_xcd) {
+    const int x = i % 8;
+    int j = i / 8;
+    if (rev) j = per_xcd - 1 - j;
+    b = 8 * (j / ips) + x;
+    k = j % ips;
+  } else {
+    b = i / ips;
+    k = i % ips;
+  }
+  u = k / S;
+  strip = k % S;
 }
 
 // ------------------------------------------------------------ user combine (U > 4)
@@ -1310,7 +1365,8 @@ __global__ __launch_bounds__(512) void k_init(BlockParams<P> prm) {
   using Real = typename P::Real;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const auto& a = prm.a;
-  const int strip = blockIdx.x, u = blockIdx.y, b = blockIdx.z;
+  int b, u, strip;
+  work_item(blockIdx.x, prm.a.B, prm.a.U, prm.strips, prm.order_rev, b, u, strip);
   const int U = a.U;
   const int m = prm.m;
   Real wm = (Real)1;
@@ -1325,7 +1381,8 @@ __global__ __launch_bounds__(512) void k_init(BlockParams<P> prm) {
 template <class P, int CHP, int TAILM>
 __global__ __launch_bounds__(512) void k_update(BlockParams<P> prm) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int strip = blockIdx.x, u = blockIdx.y, b = blockIdx.z;
+  int b, u, strip;
+  work_item(blockIdx.x, prm.a.B, prm.a.U, prm.strips, prm.order_rev, b, u, strip);
   stamp(0);
   update_user<P, CHP, TAILM>(prm, smem, b, u, strip);
   stamp(5);
@@ -1372,6 +1429,8 @@ struct Launch {
     BlockParams<P> bp;
     bp.a = args;
     bp.inline_combine = args.U <= kInlineUsers;
+    bp.strips = strips;
+    int launch_no = 0;
     // U > kInlineUsers: the leave-one-out combine runs as its own launch on the sp rows
     auto combine = [&](typename P::S* sp) {
       if (bp.inline_combine) return;
@@ -1388,7 +1447,7 @@ struct Launch {
     k_norm<<<args.B, 256, 0, st>>>(args.y, args.F * kT * 2 * args.A, args.norm);
     E_(K_NORM);
     // StateInit -> s_out; tail of the last StateInit launch: aggregation of iteration 0
-    dim3 grid(strips, args.U, args.B);
+    const dim3 grid(strips * args.U * args.B);
     B_(K_INIT);
     for (int m = 0; m < args.num_init; ++m) {
       for (int l = 0; l < 3; ++l) bp.w[l] = W.init[m][l];
@@ -1397,6 +1456,7 @@ struct Launch {
       bp.agg[0] = W.agg[0][0];
       bp.agg[1] = W.agg[0][1];
       const bool tl = bp.tail == TAIL_AGG;
+      bp.order_rev = launch_no++ & 1;
       // antenna block padding A2P (must match nrx_api.cpp init_a2p)
       if (2 * args.A <= 8) launch_init<8>(grid, L, st, bp, tl);
       else if (2 * args.A <= 16) launch_init<16>(grid, L, st, bp, tl);
@@ -1414,6 +1474,7 @@ struct Launch {
         bp.agg[0] = W.agg[i + 1][0];
         bp.agg[1] = W.agg[i + 1][1];
       }
+      bp.order_rev = launch_no++ & 1;
       B_(K_UPDATE);
 #ifdef NRX_STAMPS
       {

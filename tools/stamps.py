@@ -40,3 +40,7 @@ for L in range(3):
     seg = np.diff(det[:, L, :], axis=1)
     print(f"  conv{L + 1}: math {seg[:, 0].mean():7.0f}  bar1 {seg[:, 1].mean():7.0f}  "
           f"post {seg[:, 2].mean():7.0f}  epi {seg[:, 3].mean():7.0f}")
+z = buf[:, [0, 24, 25, 26, 27, 1]].astype(np.int64)
+zd = np.diff(z, axis=1)
+print(f"  z-load: issue {zd[:, 0].mean():7.0f}  zero-fill {zd[:, 1].mean():7.0f}  wait+store {zd[:, 2].mean():7.0f}  "
+      f"w-store {zd[:, 3].mean():7.0f}  barrier {zd[:, 4].mean():7.0f}")
