@@ -351,11 +351,10 @@ struct DenseStage {
 // pointwise A fragment are loaded once per K chunk and reused over the R rows; the three
 // input rows of consecutive outputs overlap, so a pass reads R + 2 activation rows
 // instead of 3 R.
-template <class P, int CINP, int COUTP, bool FIRST, class WS>
-__device__ __forceinline__ void conv_chunk(const char* X, const int (&rb)[P::R + 2], int sw, int kc, int g,
-                                           int lane, const WS& ws, typename P::Acc (&acc)[P::R][COUTP / 16]) {
+template <class P, int CINP, int COUTP, bool FIRST, int R, class WS>
+__device__ __forceinline__ void conv_chunk(const char* X, const int (&rb)[R + 2], int sw, int kc, int g,
+                                           int lane, const WS& ws, typename P::Acc (&acc)[R][COUTP / 16]) {
   using DV = typename P::DV;
-  constexpr int R = P::R;
   const int off = ((kc * 4 + g) ^ sw) * 16;
   DV xs[R + 2];
 #pragma unroll
@@ -380,11 +379,10 @@ __device__ __forceinline__ void conv_chunk(const char* X, const int (&rb)[P::R +
   }
 }
 
-template <class P, int CINP, int COUTP, class WS>
+template <class P, int CINP, int COUTP, int R, class WS>
 __device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int t, int g, int lane,
                                           const WS& ws,
-                                          typename P::Acc (&acc)[P::R][COUTP / 16]) {
-  constexpr int R = P::R;
+                                          typename P::Acc (&acc)[R][COUTP / 16]) {
   constexpr int NQ = CINP * (int)sizeof(typename P::S) / 16;
   constexpr int NKC = CINP / P::KC;
   const int sw = swz<NQ>(t);
@@ -395,55 +393,78 @@ __device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int
     sl = sl < 0 ? 0 : (sl >= nslots ? nslots - 1 : sl);
     rb[i] = sl * slot_pitch<P>() + t * NQ * 16;
   }
-  conv_chunk<P, CINP, COUTP, true>(X, rb, sw, 0, g, lane, ws, acc);
-  for (int kc = 1; kc < NKC; ++kc) conv_chunk<P, CINP, COUTP, false>(X, rb, sw, kc, g, lane, ws, acc);
+  conv_chunk<P, CINP, COUTP, true, R>(X, rb, sw, 0, g, lane, ws, acc);
+  for (int kc = 1; kc < NKC; ++kc) conv_chunk<P, CINP, COUTP, false, R>(X, rb, sw, kc, g, lane, ws, acc);
 }
 
-// One layer over output positions [pos_lo, pos_hi) in rounds of 8 waves x R rows.  Every
-// round computes into registers, then (after a barrier) hands the accumulators to `epi`,
-// which may overwrite input slots of rows this round consumed (in-place layers: the
-// output of position p goes to slot p - in_off - 1, which no later round reads).
+// One pass of a layer for one wave: R output rows from position p0 (act: any row valid).
+// Every pass computes into registers, then hands the accumulators to `epi`, which may
+// overwrite input slots of rows this round consumed (in-place layers: the output of
+// position p goes to slot p - in_off - 1, which no later round reads).  All waves execute
+// the same barriers.
+template <class P, int CINP, int COUTP, int R, class WS, class Epi, class Post>
+__device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off, int p0, bool act, bool first_round,
+                                           const WS& ws, Epi& epi, Post& post_math) {
+  using E = std::decay_t<Epi>;
+  const int lane = threadIdx.x & 63;
+  const int t = lane & 15, g = lane >> 4;
+  typename P::Acc acc[R][COUTP / 16];
+  typename E::template PrefT<R> pf;
+  stamp(8 + 5 * in_off);
+  if (act) epi.template prefetch<R>(pf, p0, t, g);   // epilogue global loads, in flight during the math
+  if (act) {
+    if constexpr (NRX_ABLATE & 1) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int n = 0; n < COUTP / 16; ++n) acc[r][n] = ws.bias_acc(n, g);
+    } else {
+      conv_rows<P, CINP, COUTP, R>(X, p0 - in_off, nslots, t, g, lane, ws, acc);
+    }
+  }
+  stamp(9 + 5 * in_off);
+  if constexpr (E::kNoBarrier) {
+    // the epilogue neither writes LDS nor reads anything staged after the math: each
+    // wave runs it as soon as its own math is done (post_math is empty for these)
+    if (act) epi.template run<R>(acc, pf, p0, t, g, 0, R);
+    stamp(12 + 5 * in_off);
+  } else {
+    // rows r >= kEarlyRow of an in-place layer land in slots no other wave reads this
+    // round (wave w-1 reads up to slot p0 - in_off): written before the barrier
+    constexpr int ER = E::kEarlyRow < R ? E::kEarlyRow : R;
+    if (act) epi.template run<R>(acc, pf, p0, t, g, ER, R);
+    __syncthreads();
+    stamp(10 + 5 * in_off);
+    if (first_round) post_math();      // all threads: this layer's weights are dead (P16)
+    epi.pre();                       // all threads (e.g. stage tail weights into X)
+    stamp(11 + 5 * in_off);
+    if (act) epi.template run<R>(acc, pf, p0, t, g, 0, ER);
+    stamp(12 + 5 * in_off);
+    __syncthreads();
+  }
+}
+
+// One layer over output positions [pos_lo, pos_hi).  f16 policy: one round; the rows are
+// split 4 / 3 per wave so that the 4 SIMDs (waves w and w + 4 share one) carry equal row
+// counts (28 rows: 7 per SIMD; 26: 7,7,6,6; 24: 6 each) instead of whole waves idling.
+// f64 policy: rounds of 8 waves x P::R rows.
 template <class P, int CINP, int COUTP, class WS, class Epi, class Post>
 __device__ __forceinline__ void conv_layer(const char* X, int nslots, int in_off, int pos_lo,
                                            int pos_hi, const WS& ws, Epi&& epi, Post&& post_math) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int t = lane & 15, g = lane >> 4;
-  for (int base = pos_lo; base < pos_hi; base += 8 * P::R) {
-    const int p0 = base + wave * P::R;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if constexpr (P::WLDS) {
+    static_assert(P::R == 4, "f16 row split assumes passes of 4 / 3 rows");
+    const int nrows = pos_hi - pos_lo;   // <= 32 (static_assert on FO)
+    int n4 = nrows - 24;
+    n4 = n4 < 0 ? 0 : n4;
+    const int p0 = pos_lo + 4 * (wave < n4 ? wave : n4) + 3 * (wave > n4 ? wave - n4 : 0);
     const bool act = p0 < pos_hi;
-    typename P::Acc acc[P::R][COUTP / 16];
-    typename std::decay_t<Epi>::Pref pf;
-    stamp(8 + 5 * in_off);
-    if (act) epi.prefetch(pf, p0, t, g);     // epilogue global loads, in flight during the math
-    if (act) {
-      if constexpr (NRX_ABLATE & 1) {
-#pragma unroll
-        for (int r = 0; r < P::R; ++r)
-#pragma unroll
-          for (int n = 0; n < COUTP / 16; ++n) acc[r][n] = ws.bias_acc(n, g);
-      } else {
-        conv_rows<P, CINP, COUTP>(X, p0 - in_off, nslots, t, g, lane, ws, acc);
-      }
-    }
-    stamp(9 + 5 * in_off);
-    using E = std::decay_t<Epi>;
-    if constexpr (E::kNoBarrier) {
-      // the epilogue neither writes LDS nor reads anything staged after the math: each
-      // wave runs it as soon as its own math is done (post_math is empty for these)
-      if (act) epi(acc, pf, p0, t, g, 0, P::R);
-      stamp(12 + 5 * in_off);
-    } else {
-      // rows r >= kEarlyRow of an in-place layer land in slots no other wave reads this
-      // round (wave w-1 reads up to slot p0 - in_off): written before the barrier
-      if (act) epi(acc, pf, p0, t, g, E::kEarlyRow, P::R);
-      __syncthreads();
-      stamp(10 + 5 * in_off);
-      if (base == pos_lo) post_math();   // all threads: this layer's weights are dead (P16)
-      epi.pre();                       // all threads (e.g. stage tail weights into X)
-      stamp(11 + 5 * in_off);
-      if (act) epi(acc, pf, p0, t, g, 0, E::kEarlyRow);
-      stamp(12 + 5 * in_off);
-      __syncthreads();
+    if (wave < n4) layer_pass<P, CINP, COUTP, 4>(X, nslots, in_off, p0, act, true, ws, epi, post_math);
+    else layer_pass<P, CINP, COUTP, 3>(X, nslots, in_off, p0, act, true, ws, epi, post_math);
+  } else {
+    for (int base = pos_lo; base < pos_hi; base += 8 * P::R) {
+      const int p0 = base + wave * P::R;
+      layer_pass<P, CINP, COUTP, P::R>(X, nslots, in_off, p0, p0 < pos_hi, base == pos_lo, ws, epi, post_math);
     }
   }
 }
@@ -455,21 +476,24 @@ struct NoPref {};
 // block and stay zero (P16); P64 writes them as zeros.
 template <class P, int COUTP, class WS>
 struct EpiInPlace {
-  using Pref = NoPref;
+  template <int R>
+  using PrefT = NoPref;
   static constexpr bool kNoBarrier = false;
-  static constexpr int kEarlyRow = 2 < P::R ? 2 : P::R;
+  static constexpr int kEarlyRow = 2;
   char* X;
   int in_off, pos_hi, f_start, F;
   WS ws;
   __device__ void pre() const {}
-  __device__ void prefetch(Pref&, int, int, int) const {}
-  __device__ void operator()(const typename P::Acc (&acc)[P::R][COUTP / 16], const Pref&, int p0, int t,
-                             int g, int r_lo, int r_hi) const {
+  template <int R>
+  __device__ void prefetch(NoPref&, int, int, int) const {}
+  template <int R>
+  __device__ void run(const typename P::Acc (&acc)[R][COUTP / 16], const NoPref&, int p0, int t,
+                      int g, int r_lo, int r_hi) const {
     using Real = typename P::Real;
     using S = typename P::S;
     constexpr int NQ = COUTP * (int)sizeof(S) / 16;
 #pragma unroll
-    for (int r = 0; r < P::R; ++r) {
+    for (int r = 0; r < R; ++r) {
       if (r < r_lo || r >= r_hi) continue;
       const int p = p0 + r;
       if (p >= pos_hi) continue;
@@ -734,15 +758,15 @@ template <class P, class WS, int CHP, int TAILM>
 struct EpiConv3 {
   using S = typename P::S;
   using Real = typename P::Real;
-  static constexpr int R = P::R;
   static constexpr int NTS = kDSP / 16;        // state tiles (64 channels, >= 56 are 0)
   // previous state rows, kept in storage precision (packed) until the epilogue
-  struct Pref {
+  template <int R>
+  struct PrefT {
     std::conditional_t<sizeof(S) == 2, half4, Real[4]> prev[R][NTS];
   };
   // no LDS writes; the readout tail reads head weights staged into X after the math
   static constexpr bool kNoBarrier = TAILM != TAIL_READOUT;
-  static constexpr int kEarlyRow = P::R;   // readout: every row after the barrier
+  static constexpr int kEarlyRow = 8;      // readout: every row after the barrier
   const BlockParams<P>* prm;
   char* X;
   char* WB;
@@ -753,7 +777,8 @@ struct EpiConv3 {
 
   __device__ bool row_ok(int p, int t) const { return p < pos_hi && f_start + p < prm->a.F && t < kT; }
 
-  __device__ void prefetch(Pref& pf, int p0, int t, int g) const {
+  template <int R>
+  __device__ void prefetch(PrefT<R>& pf, int p0, int t, int g) const {
     const auto& a = prm->a;
     const bool need = mode == 0 || !first;
 #pragma unroll
@@ -825,8 +850,9 @@ struct EpiConv3 {
     dense_rows<P, kHID / 16, NO * 16, RB>(hb, w2, lane, g, o, false);
   }
 
-  __device__ void operator()(const typename P::Acc (&acc)[R][NTS], const Pref& pf, int p0, int t, int g,
-                             int r_lo, int r_hi) const {
+  template <int R>
+  __device__ void run(const typename P::Acc (&acc)[R][NTS], const PrefT<R>& pf, int p0, int t, int g,
+                      int r_lo, int r_hi) const {
     if (r_lo >= r_hi) return;        // all R rows in one call
     stamp(6);
     const auto& a = prm->a;
@@ -924,7 +950,7 @@ struct EpiConv3 {
       }
     } else {
       // readouts: LLR head(s) then ChEst, RB rows at a time
-      constexpr int RB = R >= 2 ? 2 : 1;
+      constexpr int RB = R % 2 == 0 ? 2 : (R == 3 ? 3 : 1);
 #pragma unroll
       for (int r0 = 0; r0 < R; r0 += RB) {
         CFrag<P, NTS> sbr[RB];
