@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-latency", action="store_true")
+    p.add_argument("--graph", action="store_true",
+                   help="time replays of a captured hipGraph instead of direct nrx_forward calls")
     p.add_argument("--profile-only", action="store_true",
                    help="run warmup + timed steps only (for rocprofv3)")
     return p.parse_args()
@@ -86,8 +88,25 @@ def main():
     y, h, act, pe = t(slots.y), t(slots.h_hat), t(slots.active), t(pe_np)
     out = eng.alloc_outputs(B, U, F)
 
-    def step():
+    def step_eager():
         eng.forward(y, pe, h, act, None, num_it, args.precision, out=out)
+
+    # The timed steps are direct nrx_forward calls (async, no host sync: the host runs ahead
+    # of the device); --graph replays one captured forward instead (measured slower at this
+    # batch: a replay costs more than three back-to-back launches).
+    graph_stream = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(graph_stream):
+        for _ in range(max(args.warmup, 3)):
+            step_eager()
+    torch.cuda.synchronize()
+    if not args.graph:
+        step = step_eager
+    else:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=graph_stream):
+            step_eager()
+        torch.cuda.synchronize()
+        step = graph.replay
 
     for _ in range(args.warmup):
         step()
@@ -122,7 +141,7 @@ def main():
     re_users = B * U * F * 14
     eng.profile(True)
     for _ in range(args.steps):
-        step()
+        step_eager()
     prof = eng.profile_read()
     eng.profile(False)
     kern = {}
@@ -181,7 +200,8 @@ def main():
             "data": "synthetic (seeded PUSCH slots: 16-QAM, DMRS type 1, TDL channel, LS+NN h_hat; trained nrx_rt weights)",
             "config": {"workload": f"{args.config}, {U} users, {args.prbs} PRB, 4 rx_ant, 16-QAM, "
                                    f"batch={B} slots per GPU",
-                       "global_batch": B * world, "num_it": num_it, "parallelism": f"dp{world} (slot shards)"},
+                       "global_batch": B * world, "num_it": num_it, "parallelism": f"dp{world} (slot shards)",
+                       "launch": "hipGraph replay of nrx_forward" if args.graph else "direct nrx_forward calls"},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "p50_latency_ms": latency,

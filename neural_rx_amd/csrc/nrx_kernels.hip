@@ -4,9 +4,10 @@
 // the TF structure of "neural_rx copy_pytorch.py" (StateInit :82-188, AggregateUserStates
 // :191-231, UpdateState :234-287, ReadoutLLRs/ChEst :324-362).
 //
-// Kernel map (per forward: 1 + M_init + num_it launches):
-//   k_norm      per-slot 1/sqrt(mean(y^2)), divide-no-nan        (neural_rx.py:551-557)
+// Kernel map (per forward: M_init + num_it launches):
 //   k_init      StateInit: z=[y,pe,h] -> 3 separable convs       (copy_pytorch.py:160-188)
+//               the slot normalisation 1/sqrt(mean(y^2)) (neural_rx.py:551-557) is computed
+//               in its prologue (slot_norm)
 //               one launch per init head m, accumulating the Var-IO mcs mix
 //               (neural_rx.py:562-569); the last one runs the aggregation MLP of
 //               iteration 0 in its conv3 epilogue and the leave-one-out user combine
@@ -573,34 +574,6 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// ======================================================================== k_norm
-// ns[b] = 1/sqrt(mean(y[b]^2)) over the whole provided grid (F x T x 2A);
-// divide-no-nan: an all-zero slot gets 0.
-__global__ __launch_bounds__(256) void k_norm(const float* __restrict__ y, int n_per_slot,
-                                              double* __restrict__ ns) {
-  __shared__ double red[256];
-  const float* p = y + (size_t)blockIdx.x * n_per_slot;
-  double acc = 0.0;
-  for (int i = threadIdx.x * 4; i < n_per_slot; i += 256 * 4) {
-    if (i + 3 < n_per_slot) {
-      const floatx4 v = *reinterpret_cast<const floatx4*>(p + i);
-      acc += (double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2] + (double)v[3] * v[3];
-    } else {
-      for (int k = i; k < n_per_slot; ++k) acc += (double)p[k] * p[k];
-    }
-  }
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const double ms = red[0] / (double)n_per_slot;
-    ns[blockIdx.x] = ms > 0.0 ? 1.0 / sqrt(ms) : 0.0;
-  }
-}
-
 // ===================================================== separable-conv block kernels
 // One workgroup = one (slot, user, subcarrier strip) running the 3-conv block of the
 // state init or of one iteration's state update.  The per-user MLPs that consume the new
@@ -1105,9 +1078,32 @@ constexpr int init_cinp(int kc) {
   return p;
 }
 
+// Slot normalisation (neural_rx.py:551-557): ns = 1/sqrt(mean(y^2)) over the whole grid
+// given (F x 14 x 2A floats, nq float4s), divide-no-nan (an all-zero slot gets 0).  Every
+// workgroup of the slot computes it (21 KB at nrx_rt, L2-resident after the first): no
+// separate launch.  Double accumulation; `red` is 8 doubles of LDS.
+__device__ __forceinline__ double slot_norm(const float* y, int nq, double* red) {
+  const floatx4* yq = reinterpret_cast<const floatx4*>(y);
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nq; i += 512) {
+    const floatx4 v = yq[i];
+    acc += (double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2] + (double)v[3] * v[3];
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  double tot = 0.0;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) tot += red[w];
+  const double ms = tot / (double)(4 * nq);
+  return ms > 0.0 ? 1.0 / sqrt(ms) : 0.0;
+}
+
 template <class P, int A2P, int CHP, int TAILM>
 __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem, int b, int u,
                                           int strip, typename P::Real wm, bool first) {
+  __shared__ double red[8];
   using S = typename P::S;
   using Real = typename P::Real;
   constexpr int CINP = init_cinp<A2P>(P::KC);
@@ -1119,7 +1115,6 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
   const int f_start = f0 - kHalo;
   char* X = smem;
   char* WB = smem + R0 * slot_pitch<P>();
-  const Real ns = (Real)a.norm[b];
   if constexpr (sizeof(S) == 2 && CINP < kHID) {
     // pad symbols t = 14, 15 of the 128-channel layout the conv layers write in place:
     // zero once (the z image below occupies the first CINP*32 bytes of each slot)
@@ -1154,6 +1149,7 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
       hv[2 * k + 1] = w.y;
     }
     if (ok) pv = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + f) * kT + tt) * 2);
+    const Real ns = (Real)slot_norm(a.y + (size_t)b * F * kT * A2, F * kT * A2 / 4, red);
     if (lf < R0) {
 #pragma unroll
       for (int q = 0; q < NQZ; ++q) {
@@ -1469,9 +1465,6 @@ struct Launch {
     }
     bp.chest[0] = W.chest[0];
     bp.chest[1] = W.chest[1];
-    B_(K_NORM);
-    k_norm<<<args.B, 256, 0, st>>>(args.y, args.F * kT * 2 * args.A, args.norm);
-    E_(K_NORM);
     // StateInit -> s_out; tail of the last StateInit launch: aggregation of iteration 0
     const dim3 grid(strips * args.U * args.B);
     B_(K_INIT);
