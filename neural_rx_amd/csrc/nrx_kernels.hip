@@ -487,6 +487,11 @@ struct EpiInPlace {
   __device__ void pre() const {}
   template <int R>
   __device__ void prefetch(NoPref&, int, int, int) const {}
+  // byte offset of lane (t, g)'s 4 channels of tile n inside a slot (f16 layout)
+  __device__ static int lane_off(int n, int t, int g) {
+    constexpr int NQ = COUTP * 2 / 16;
+    return xoff<P, NQ>(0, t, 2 * n + (g >> 1)) + (g & 1) * 8;
+  }
   template <int R>
   __device__ void run(const typename P::Acc (&acc)[R][COUTP / 16], const NoPref&, int p0, int t,
                       int g, int r_lo, int r_hi) const {
@@ -502,13 +507,21 @@ struct EpiInPlace {
       const bool z = f < 0 || f >= F;
       const int slot = p - in_off - 1;
       if constexpr (sizeof(S) == 2) {
+        // p0 (hence p, f, z, slot) is wave-uniform: the grid-edge test is a scalar branch,
+        // and the row's slot offset is added to per-tile lane offsets computed once
+        char* row = X + slot * slot_pitch<P>();
         if (t < kT) {
+          if (!z) {
 #pragma unroll
-          for (int n = 0; n < COUTP / 16; ++n) {
-            half4 h = half4{(S)acc[r][n][0], (S)acc[r][n][1], (S)acc[r][n][2], (S)acc[r][n][3]};
-            h = __builtin_elementwise_max(h, half4{0, 0, 0, 0});
-            if (z) h = half4{0, 0, 0, 0};
-            *reinterpret_cast<half4*>(X + xoff<P, NQ>(slot, t, 2 * n + (g >> 1)) + (g & 1) * 8) = h;
+            for (int n = 0; n < COUTP / 16; ++n) {
+              half4 h = half4{(S)acc[r][n][0], (S)acc[r][n][1], (S)acc[r][n][2], (S)acc[r][n][3]};
+              h = __builtin_elementwise_max(h, half4{0, 0, 0, 0});
+              *reinterpret_cast<half4*>(row + lane_off(n, t, g)) = h;
+            }
+          } else {
+#pragma unroll
+            for (int n = 0; n < COUTP / 16; ++n)
+              *reinterpret_cast<half4*>(row + lane_off(n, t, g)) = half4{0, 0, 0, 0};
           }
         }
       } else {
@@ -1170,7 +1183,9 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
   }
   if constexpr (P::WLDS) w1.store(WB);
   __syncthreads();
+  stamp(1);
   strip_block<P, CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 1, wm, first);
+  stamp(4);
 }
 
 // UpdateState of user u on the strip (z = [a, s, pe]).
@@ -1396,7 +1411,9 @@ __global__ __launch_bounds__(512) void k_init(BlockParams<P> prm) {
     wm = a.mcs_mask ? (Real)a.mcs_mask[((size_t)b * U + u) * a.M + m] : (Real)(m == 0 ? 1 : 0);
   // wm == 0: this MCS contributes exactly 0 * finite; the conv math is still run (the
   // m = 0 launch defines s, the last launch applies the aggregation MLP).
+  stamp(0);
   init_user<P, A2P, 16, TAILM>(prm, smem, b, u, strip, wm, m == 0);
+  stamp(5);
 }
 
 // UpdateState of one (slot, user, strip) with the fused tail.  grid = (strips, U, B).
@@ -1476,6 +1493,14 @@ struct Launch {
       bp.agg[1] = W.agg[0][1];
       const bool tl = bp.tail == TAIL_AGG;
       bp.order_rev = launch_no++ & 1;
+#ifdef NRX_STAMPS
+      {
+        static const int sel = getenv("NRX_STAMP_LAUNCH") ? atoi(getenv("NRX_STAMP_LAUNCH")) : 0;
+        const int on = sel == -1 - m;
+        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_nrx_stamp_on), &on, sizeof(int), 0, hipMemcpyHostToDevice, st);
+        (void)hipStreamSynchronize(st);
+      }
+#endif
       // antenna block padding A2P (must match nrx_api.cpp init_a2p)
       if (2 * args.A <= 8) launch_init<8>(grid, L, st, bp, tl);
       else if (2 * args.A <= 16) launch_init<16>(grid, L, st, bp, tl);

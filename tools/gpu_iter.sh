@@ -10,4 +10,5 @@ timeout -k 10 300 python bench.py --no-cpu-baseline --no-latency > $O/bench.json
 python -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], {k: v['avg_us'] for k, v in d['kernels'].items()}, d['roofline']['frac'])"
 timeout -k 10 300 python tools/stamps.py 2>&1 | grep -v amdgpu.ids > $O/stamps.log
 NRX_STAMP_LAUNCH=1 timeout -k 10 300 python tools/stamps.py 2>&1 | grep -v amdgpu.ids >> $O/stamps.log
+NRX_STAMP_LAUNCH=-1 timeout -k 10 300 python tools/stamps.py 2>&1 | grep -v amdgpu.ids >> $O/stamps.log
 cat $O/stamps.log

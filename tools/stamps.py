@@ -28,7 +28,7 @@ st = buf[:, [0, 1, 2, 3, 6, 4, 5]].astype(np.int64)
 d = np.diff(st, axis=1)
 names = ["z-load", "conv1", "conv2", "conv3", "epilogue", "tail"]
 launch = os.environ.get("NRX_STAMP_LAUNCH", "0")
-print("k_update launch", os.environ.get("NRX_STAMP_LAUNCH", "0"))
+print("launch", os.environ.get("NRX_STAMP_LAUNCH", "0"), "(k_update i; -1 = k_init)")
 tot = st[:, -1] - st[:, 0]
 print("cycles per WG (mean):", tot.mean(), " start spread:", st[:, 0].max() - st[:, 0].min())
 for i, nm in enumerate(names):
