@@ -805,6 +805,38 @@ struct EpiConv3 {
     }
   }
 
+  // f16 state row (56 channels of one (f, t)) from the C layout of the 4 state tiles: lane
+  // (t, g) holds channels 16n + 4g .. +3 of tile n.  v_permlane16_swap on the tile pairs
+  // (0,1) and (2,3) exchanges the 16-lane rows g <-> g^1 so that every lane holds 16
+  // contiguous bytes per pair (8-channel chunk 2n + 2(g&1) + (g>>1)): two 16-byte stores
+  // per lane instead of four 8-byte ones (chunk 7, channels 56..63, is padding and not
+  // stored).  The swaps run on every lane; only the stores are predicated.
+  __device__ static void store_row16(S* dst, const Real (&v)[NTS][4], bool ok, int g) {
+    unsigned w[NTS][2];
+#pragma unroll
+    for (int n = 0; n < NTS; ++n) {
+      const half2 lo = half2{(S)v[n][0], (S)v[n][1]}, hi = half2{(S)v[n][2], (S)v[n][3]};
+      w[n][0] = __builtin_bit_cast(unsigned, lo);
+      w[n][1] = __builtin_bit_cast(unsigned, hi);
+    }
+#pragma unroll
+    for (int n = 0; n < NTS; n += 2)
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const auto x = __builtin_amdgcn_permlane16_swap(w[n][d], w[n + 1][d], false, false);
+        w[n][d] = x[0];
+        w[n + 1][d] = x[1];
+      }
+    if (!ok) return;
+    const int ck = 2 * (g & 1) + (g >> 1);
+#pragma unroll
+    for (int n = 0; n < NTS; n += 2) {
+      const int chunk = 2 * n + ck;
+      if (chunk * 8 < kDS)
+        *reinterpret_cast<intx4*>(dst + chunk * 8) = intx4{(int)w[n][0], (int)w[n][1], (int)w[n + 1][0], (int)w[n + 1][1]};
+    }
+  }
+
   // store NT16 tiles of f32 outputs for one row: channel co = 16 n + P::co(g, j) < nvalid
   template <int NT16>
   __device__ __forceinline__ void store_f32(float* dst, const Real (&o)[NT16][4], int g, int nvalid) const {
@@ -869,17 +901,11 @@ struct EpiConv3 {
     if constexpr (TAILM != TAIL_READOUT) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        if (!ok[r]) continue;
         S* dst = a.s_out + off[r];
         if constexpr (sizeof(S) == 2) {
-#pragma unroll
-          for (int n = 0; n < NTS; ++n) {
-            const int c0 = 16 * n + 4 * g;
-            if (c0 < kDS)
-              *reinterpret_cast<half4*>(dst + c0) =
-                  half4{(S)sv[r][n][0], (S)sv[r][n][1], (S)sv[r][n][2], (S)sv[r][n][3]};
-          }
+          store_row16(dst, sv[r], ok[r], g);
         } else {
+          if (!ok[r]) continue;
 #pragma unroll
           for (int n = 0; n < NTS; ++n)
 #pragma unroll
@@ -914,17 +940,16 @@ struct EpiConv3 {
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        if (!ok[r]) continue;
         S* dst = a.a_out + off[r];
         if constexpr (sizeof(S) == 2) {
+          Real spa[NTS][4];
 #pragma unroll
-          for (int n = 0; n < NTS; ++n) {
-            const int c0 = 16 * n + 4 * g;
-            if (c0 < kDS)
-              *reinterpret_cast<half4*>(dst + c0) = half4{(S)(sp[r][n][0] * act), (S)(sp[r][n][1] * act),
-                                                          (S)(sp[r][n][2] * act), (S)(sp[r][n][3] * act)};
-          }
+          for (int n = 0; n < NTS; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) spa[n][j] = sp[r][n][j] * act;
+          store_row16(dst, spa, ok[r], g);
         } else {
+          if (!ok[r]) continue;
 #pragma unroll
           for (int n = 0; n < NTS; ++n)
 #pragma unroll
