@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NRX_API_VERSION 1
+#define NRX_API_VERSION 2
 
 enum nrx_status {
   NRX_OK = 0,
@@ -117,6 +117,48 @@ int nrx_forward(nrx_handle* h, const nrx_io* io, void* workspace, size_t workspa
                 void* stream);
 
 void nrx_destroy(nrx_handle* h);
+
+/* ---------------------------------------------------------------- Aerial contract
+ * The NeuralReceiverONNX / TensorRT engine I/O (neural_rx.py:1773-1812; feed dict of
+ * notebooks/real_time_nrx.ipynb:792-844): LS channel estimates at the DMRS pilots in, the
+ * FOCC removal + per-PRB nearest-pilot interpolation + positional encoding
+ * (NRPreprocessing, neural_rx.py:1614-1711) run on the GPU, LLRs out in the Aerial layout
+ * and sign.  Single MCS, as the ONNX export (LLR head 0, mcs mask one-hot on MCS 0).
+ *   y_real, y_imag        [B][F][T][A]            f32   rx_slot_{real,imag}
+ *   h_ls_real, h_ls_imag  [B][Npil][U][A]         f32   LS estimates at the pilots,
+ *                          Npil = nsym * (F/12) * npil, pilot p = (k * F/12 + prb) * npil + j
+ *                          (DMRS symbol k, PRB, pilot j of the PRB); FOCC pairs p, p^1
+ *   dmrs_port_mask        [B][U]                  f32   active DMRS ports
+ *   dmrs_ofdm_pos         [U][nsym]               i32   DMRS symbol indices (device)
+ *   dmrs_subcarrier_pos   [U][npil]               i32   pilot subcarriers within a PRB (device)
+ *   llr                   [B][bits][U][F][T]      f32   out, LLR = log p(b=0)/p(b=1)
+ *   h_hat                 [B][U][F][T][2A]        f32   out, refined estimate (NULL: skip)
+ */
+typedef struct nrx_aerial_io {
+  nrx_shape shape;           /* B, U = num_tx, F (multiple of 12), T = 14 */
+  int32_t num_it;
+  int32_t precision;
+  int32_t num_dmrs_symbols;  /* nsym */
+  int32_t num_dmrs_subcarriers; /* npil (even; 6 for DMRS type 1) */
+  const float* y_real;
+  const float* y_imag;
+  const float* h_ls_real;
+  const float* h_ls_imag;
+  const float* dmrs_port_mask;
+  const int32_t* dmrs_ofdm_pos;
+  const int32_t* dmrs_subcarrier_pos;
+  float* llr;
+  float* h_hat;
+} nrx_aerial_io;
+
+/* Workspace of nrx_forward_aerial (the CGNN workspace plus the preprocessed y, h_hat, pe,
+ * NN table and the Sionna-layout LLRs). */
+int nrx_aerial_workspace_size(const nrx_handle* h, const nrx_aerial_io* io, size_t* bytes);
+
+/* Asynchronous Aerial-contract forward on `stream`; device pointers, no allocation, no
+ * host synchronisation. */
+int nrx_forward_aerial(nrx_handle* h, const nrx_aerial_io* io, void* workspace, size_t workspace_bytes,
+                       void* stream);
 
 /* Host helper: nearest-pilot positional encoding pe[U][F][T][2] for DMRS
  * configuration type 1 (restates onnx_utils.py:172-260 for the product path).

@@ -22,7 +22,7 @@ PRECISIONS = {"f16": NRX_PREC_F16, "fp16": NRX_PREC_F16, "f32x": NRX_PREC_F32X,
 EXPORTS = [
     "nrx_create", "nrx_weight_layout", "nrx_workspace_size", "nrx_forward", "nrx_destroy",
     "nrx_compute_pe", "nrx_flops_per_re_user", "nrx_last_error", "nrx_api_version",
-    "nrx_profile_enable", "nrx_profile_read",
+    "nrx_profile_enable", "nrx_profile_read", "nrx_aerial_workspace_size", "nrx_forward_aerial",
 ]
 KERNELS = ["norm", "state_init", "state_update"]
 
@@ -77,6 +77,25 @@ class nrx_io(ctypes.Structure):
     ]
 
 
+class nrx_aerial_io(ctypes.Structure):
+    _fields_ = [
+        ("shape", nrx_shape),
+        ("num_it", ctypes.c_int32),
+        ("precision", ctypes.c_int32),
+        ("num_dmrs_symbols", ctypes.c_int32),
+        ("num_dmrs_subcarriers", ctypes.c_int32),
+        ("y_real", ctypes.c_void_p),
+        ("y_imag", ctypes.c_void_p),
+        ("h_ls_real", ctypes.c_void_p),
+        ("h_ls_imag", ctypes.c_void_p),
+        ("dmrs_port_mask", ctypes.c_void_p),
+        ("dmrs_ofdm_pos", ctypes.c_void_p),
+        ("dmrs_subcarrier_pos", ctypes.c_void_p),
+        ("llr", ctypes.c_void_p),
+        ("h_hat", ctypes.c_void_p),
+    ]
+
+
 _lib = None
 
 
@@ -124,6 +143,10 @@ def load(path: str = LIB_PATH):
     lib.nrx_profile_enable.restype = c.c_int
     lib.nrx_profile_read.argtypes = [c.c_void_p, c.c_int32, P(c.c_int64), P(c.c_double)]
     lib.nrx_profile_read.restype = c.c_int
+    lib.nrx_aerial_workspace_size.argtypes = [c.c_void_p, P(nrx_aerial_io), P(c.c_size_t)]
+    lib.nrx_aerial_workspace_size.restype = c.c_int
+    lib.nrx_forward_aerial.argtypes = [c.c_void_p, P(nrx_aerial_io), c.c_void_p, c.c_size_t, c.c_void_p]
+    lib.nrx_forward_aerial.restype = c.c_int
     lib.nrx_api_version.argtypes = []
     lib.nrx_api_version.restype = c.c_int32
     _lib = lib

@@ -482,6 +482,108 @@ int nrx_forward(nrx_handle* h, const nrx_io* io, void* workspace, size_t workspa
   return NRX_OK;
 }
 
+// ---------------------------------------------------------------- Aerial contract
+namespace {
+struct AerialWs {
+  float* y;
+  float* h;
+  float* pe;
+  int32_t* nn;
+  float* llr;
+  void* cgnn;
+  size_t cgnn_bytes;
+  size_t total;
+};
+
+AerialWs aerial_layout(const nrx_handle* h, const nrx_aerial_io* io, void* base, size_t cgnn_bytes) {
+  const nrx_shape& s = io->shape;
+  const size_t A2 = 2 * (size_t)h->desc.num_rx_ant;
+  const size_t re = (size_t)s.num_subcarriers * s.num_symbols;
+  AerialWs w{};
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off += align256(bytes);
+    return (char*)base + o;
+  };
+  w.y = (float*)take((size_t)s.batch * re * A2 * 4);
+  w.h = (float*)take((size_t)s.batch * s.num_tx * re * A2 * 4);
+  w.pe = (float*)take((size_t)s.num_tx * re * 2 * 4);
+  w.nn = (int32_t*)take((size_t)s.num_tx * s.num_symbols * 12 * 4);
+  w.llr = (float*)take((size_t)num_heads(&h->desc) * s.batch * s.num_tx * re * bits_max(&h->desc) * 4);
+  w.cgnn = take(cgnn_bytes);
+  w.cgnn_bytes = cgnn_bytes;
+  w.total = off;
+  return w;
+}
+
+int check_aerial(const nrx_handle* h, const nrx_aerial_io* io) {
+  if (!h || !io) return fail(NRX_ERR_INVALID_ARG, "null argument");
+  int rc = check_shape(&io->shape);
+  if (rc) return rc;
+  if (io->shape.num_subcarriers % 12) return fail(NRX_ERR_SHAPE, "num_subcarriers must be a multiple of 12 (PRBs)");
+  if (io->num_dmrs_symbols < 1 || io->num_dmrs_symbols > 14)
+    return fail(NRX_ERR_SHAPE, "num_dmrs_symbols must be 1..14");
+  if (io->num_dmrs_subcarriers < 2 || io->num_dmrs_subcarriers > 12 || io->num_dmrs_subcarriers % 2)
+    return fail(NRX_ERR_SHAPE, "num_dmrs_subcarriers must be even and 2..12 (FOCC pairs)");
+  return NRX_OK;
+}
+}  // namespace
+
+int nrx_aerial_workspace_size(const nrx_handle* h, const nrx_aerial_io* io, size_t* bytes) {
+  int rc = check_aerial(h, io);
+  if (rc) return rc;
+  if (!bytes) return fail(NRX_ERR_INVALID_ARG, "null argument");
+  size_t cg = 0;
+  rc = nrx_workspace_size(h, &io->shape, io->precision, &cg);
+  if (rc) return rc;
+  *bytes = aerial_layout(h, io, nullptr, cg).total;
+  return NRX_OK;
+}
+
+int nrx_forward_aerial(nrx_handle* h, const nrx_aerial_io* io, void* workspace, size_t workspace_bytes,
+                       void* stream) {
+  int rc = check_aerial(h, io);
+  if (rc) return rc;
+  if (!io->y_real || !io->y_imag || !io->h_ls_real || !io->h_ls_imag || !io->dmrs_port_mask ||
+      !io->dmrs_ofdm_pos || !io->dmrs_subcarrier_pos || !io->llr)
+    return fail(NRX_ERR_INVALID_ARG, "null tensor pointer");
+  size_t cg = 0;
+  rc = nrx_workspace_size(h, &io->shape, io->precision, &cg);
+  if (rc) return rc;
+  const AerialWs w = aerial_layout(h, io, workspace, cg);
+  if (!workspace || workspace_bytes < w.total)
+    return fail(NRX_ERR_WORKSPACE, "workspace too small: need " + std::to_string(w.total) + " bytes");
+  const nrx_shape& s = io->shape;
+  const int A = h->desc.num_rx_ant;
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e = launch_aerial_tables(io->dmrs_ofdm_pos, io->dmrs_subcarrier_pos, s.num_tx, io->num_dmrs_symbols,
+                                      io->num_dmrs_subcarriers, s.num_symbols, s.num_subcarriers, w.nn, w.pe, st);
+  if (e == hipSuccess)
+    e = launch_aerial_inputs(io->y_real, io->y_imag, io->h_ls_real, io->h_ls_imag, w.nn, s.batch, s.num_tx,
+                             s.num_subcarriers, s.num_symbols, A, io->num_dmrs_symbols, io->num_dmrs_subcarriers,
+                             w.y, w.h, st);
+  if (e != hipSuccess) return hip_fail(e, "aerial preprocessing launch");
+  nrx_io cio{};
+  cio.shape = s;
+  cio.num_it = io->num_it;
+  cio.precision = io->precision;
+  cio.y = w.y;
+  cio.pe = w.pe;
+  cio.h_hat = w.h;
+  cio.active = io->dmrs_port_mask;
+  cio.mcs_mask = nullptr;
+  cio.llr = w.llr;
+  cio.h_ref = io->h_hat;
+  rc = nrx_forward(h, &cio, w.cgnn, w.cgnn_bytes, stream);
+  if (rc) return rc;
+  const int bits0 = h->desc.var_mcs_masking ? bits_max(&h->desc) : h->desc.bits[0];
+  e = launch_aerial_llr(w.llr, s.batch, s.num_tx, s.num_subcarriers, s.num_symbols, bits_max(&h->desc), bits0,
+                        io->llr, st);
+  if (e != hipSuccess) return hip_fail(e, "aerial LLR layout launch");
+  return NRX_OK;
+}
+
 int nrx_profile_enable(nrx_handle* h, int32_t enable) {
   if (!h) return fail(NRX_ERR_INVALID_ARG, "null handle");
   if (enable) {

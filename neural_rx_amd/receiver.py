@@ -176,6 +176,96 @@ class CGNNEngine:
         return llr, h_ref
 
 
+    # -------------------------------------------------------------- Aerial contract
+    def forward_aerial(self, y_real, y_imag, h_ls_real, h_ls_imag, dmrs_port_mask, dmrs_ofdm_pos,
+                       dmrs_subcarrier_pos, num_it=None, precision="f16", want_h=True, stream=None):
+        """NeuralReceiverONNX I/O on the GPU (include/nrx.h, nrx_forward_aerial).
+
+        ``y_real/imag [B,F,T,A]``, ``h_ls_real/imag [B,Npil,U,A]`` (LS at the DMRS pilots,
+        pilot p = (k * F/12 + prb) * npil + j), ``dmrs_port_mask [B,U]`` float,
+        ``dmrs_ofdm_pos [U,nsym]`` / ``dmrs_subcarrier_pos [U,npil]`` int32 CUDA tensors.
+        Returns ``(llr [B,bits,U,F,T], h_hat [B,U,F,T,2A] or None)`` with the Aerial sign."""
+        torch = _torch()
+        sp = self.spec
+        B, F, T, A = y_real.shape
+        U = dmrs_port_mask.shape[1]
+        if T != NUM_SYMBOLS or A != sp.num_rx_ant:
+            raise ValueError(f"y must be [B,F,14,{sp.num_rx_ant}], got {tuple(y_real.shape)}")
+        nsym, npil = dmrs_ofdm_pos.shape[1], dmrs_subcarrier_pos.shape[1]
+        if h_ls_real.shape[1] != nsym * (F // 12) * npil or h_ls_real.shape[3] != A:
+            raise ValueError(f"h_ls must be [B,{nsym * (F // 12) * npil},U,{A}], got {tuple(h_ls_real.shape)}")
+        if h_ls_real.shape[2] != U:        # h_hat[:, 0, :, :num_tx] (neural_rx.py:1709)
+            h_ls_real, h_ls_imag = h_ls_real[:, :, :U], h_ls_imag[:, :, :U]
+        f32 = [y_real, y_imag, h_ls_real, h_ls_imag, dmrs_port_mask]
+        for t in f32:
+            if not t.is_cuda or t.dtype != torch.float32:
+                raise ValueError("y / h_ls / dmrs_port_mask must be float32 CUDA tensors")
+        pos = [dmrs_ofdm_pos[:U], dmrs_subcarrier_pos[:U]]
+        for t in pos:
+            if not t.is_cuda or t.dtype != torch.int32:
+                raise ValueError("dmrs positions must be int32 CUDA tensors")
+        y_real, y_imag, h_ls_real, h_ls_imag, mask = [t.contiguous() for t in f32]
+        ofdm, scp = [t.contiguous() for t in pos]
+        bits = sp.bits_max if sp.masking else sp.bits[0]
+        llr = torch.empty((B, bits, U, F, NUM_SYMBOLS), dtype=torch.float32, device=y_real.device)
+        h = (torch.empty((B, U, F, NUM_SYMBOLS, 2 * A), dtype=torch.float32, device=y_real.device)
+             if want_h else None)
+        io = _lib.nrx_aerial_io()
+        io.shape = _lib.nrx_shape(B, U, F, NUM_SYMBOLS)
+        io.num_it = sp.num_it if num_it is None else num_it
+        io.precision = _lib.PRECISIONS[precision]
+        io.num_dmrs_symbols, io.num_dmrs_subcarriers = nsym, npil
+        io.y_real, io.y_imag = y_real.data_ptr(), y_imag.data_ptr()
+        io.h_ls_real, io.h_ls_imag = h_ls_real.data_ptr(), h_ls_imag.data_ptr()
+        io.dmrs_port_mask = mask.data_ptr()
+        io.dmrs_ofdm_pos, io.dmrs_subcarrier_pos = ofdm.data_ptr(), scp.data_ptr()
+        io.llr = llr.data_ptr()
+        io.h_hat = h.data_ptr() if h is not None else None
+        nbytes = ctypes.c_size_t()
+        _lib.check(self._lib.nrx_aerial_workspace_size(self._h, ctypes.byref(io), ctypes.byref(nbytes)))
+        ws = self._workspace(nbytes.value)
+        if stream is None:
+            stream = torch.cuda.current_stream(y_real.device).cuda_stream
+        _lib.check(self._lib.nrx_forward_aerial(self._h, ctypes.byref(io), ws.data_ptr(), ws.numel(), stream))
+        self._last_inputs = [y_real, y_imag, h_ls_real, h_ls_imag, mask, ofdm, scp]
+        return llr, h
+
+
+class AerialReceiver:
+    """Mirror of NeuralReceiverONNX (neural_rx.py:1717-1812): the TensorRT engine's feed
+    dict (real_time_nrx.ipynb:792-844) in, ``(llr [B,bits,U,F,T], h_hat [B,U,F,T,2A])`` out,
+    LLR = log p(b=0)/p(b=1).  Single MCS, as the ONNX export."""
+
+    def __init__(self, config: str | NRXConfig = "nrx_rt", weight_list=None, device: int = 0,
+                 precision: str = "f16", num_tx: Optional[int] = None, num_rx_ant: Optional[int] = None):
+        self.cfg = get_config(config) if isinstance(config, str) else config
+        self.spec = spec_from_config(self.cfg, num_rx_ant)
+        if weight_list is None:
+            weight_list = _weights.load(self.cfg.label)
+        self.engine = CGNNEngine(self.spec, weight_list, device)
+        self.precision = precision
+        self._num_tx = num_tx or self.cfg.max_num_tx
+        self._num_it = self.cfg.num_nrx_iter_eval
+
+    @property
+    def num_it(self):
+        return self._num_it
+
+    @num_it.setter
+    def num_it(self, val):
+        assert (val >= 1) and (val <= self.spec.num_it), "Invalid number of iterations"
+        self._num_it = val
+
+    def forward(self, inputs):
+        (y_real, y_imag, h_hat_real, h_hat_imag, dmrs_port_mask, dmrs_ofdm_pos,
+         dmrs_subcarrier_pos) = inputs
+        U = self._num_tx
+        return self.engine.forward_aerial(y_real, y_imag, h_hat_real, h_hat_imag, dmrs_port_mask[:, :U],
+                                          dmrs_ofdm_pos, dmrs_subcarrier_pos, self._num_it, self.precision)
+
+    __call__ = forward
+
+
 def spec_for(config: str | NRXConfig, num_rx_ant: Optional[int] = None) -> ModelSpec:
     cfg = get_config(config) if isinstance(config, str) else config
     return spec_from_config(cfg, num_rx_ant)

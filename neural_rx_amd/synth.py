@@ -57,6 +57,7 @@ class Slots:
     data_mask: np.ndarray  # [T] bool, data-carrying symbols
     active: np.ndarray     # [B, U] float32
     y_complex: np.ndarray  # [B, 1, A, T, F] complex64 (Sionna layout)
+    x: Optional[np.ndarray] = None   # [B, U, F, T] complex64 transmitted grid (data + DMRS)
 
 
 def _tdl(rng, batch, users, ants, f, t, max_delay_s, max_doppler_hz, taps=6):
@@ -129,7 +130,8 @@ def generate(batch: int, num_users: int, num_prbs: int, num_rx_ant: int,
     y = to_ch(yc)
     return Slots(y=y, h_hat=to_ch(h_hat), h=to_ch(h), bits=bits, data_mask=data_mask,
                  active=active.astype(np.float32),
-                 y_complex=np.transpose(yc, (0, 1, 3, 2))[:, None].astype(np.complex64))
+                 y_complex=np.transpose(yc, (0, 1, 3, 2))[:, None].astype(np.complex64),
+                 x=x.astype(np.complex64))
 
 
 def hard_bits(llr: np.ndarray) -> np.ndarray:

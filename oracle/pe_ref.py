@@ -65,8 +65,10 @@ def aerial_nn_indices(dmrs_ofdm_pos: np.ndarray, dmrs_subcarrier_pos: np.ndarray
     """NRPreprocessing._calculate_nn_indices with TF semantics.
 
     Returns ``nn_idx [U, 1, T, 12]`` (index into the per-PRB pilot list ordered
-    subcarrier-major: ``i = i_sc * n_sym + i_sym``, as ``tf.meshgrid(sc, sym)``
-    with 'ij' stacking of the pilot grid in the faithful copy) and ``pe [U, F, T, 2]``.
+    symbol-major: ``i = i_sym * n_sc + i_sc``, the flattening of TF's default 'xy'
+    ``meshgrid(dmrs_subcarrier_pos, dmrs_ofdm_pos)`` of shape [n_sym, n_sc]) and
+    ``pe [U, F, T, 2]``.  Ties in the Manhattan distance go to the first pilot in that
+    order (argmin); the PE normalisation uses the population std (tf.math.reduce_std).
     """
     num_tx = dmrs_ofdm_pos.shape[0]
     # RE list in symbol-major order: TF meshgrid default 'xy' -> shape [T, 12]
@@ -99,3 +101,57 @@ def focc_removal(h_hat: np.ndarray) -> np.ndarray:
     h = h.sum(-1, keepdims=True) / 2.0
     h = np.repeat(h, 2, axis=-1)
     return h.reshape(s)
+
+
+def aerial_preprocess(y_real, y_imag, h_ls_real, h_ls_imag, dmrs_ofdm_pos, dmrs_subcarrier_pos,
+                      num_tx: int):
+    """NeuralReceiverONNX input stage with TF semantics (neural_rx.py:1773-1797 +
+    NRPreprocessing.forward 1698-1711; TF structure in "neural_rx copy_pytorch.py"
+    959-1092).
+
+    y_real/imag [B, F, T, A]; h_ls_real/imag [B, Npil, U, A] with the pilot axis ordered
+    (DMRS symbol k, PRB, pilot j): ``p = (k * nprb + prb) * n_sc + j`` (the two
+    ``split_dim`` calls of ``_nn_interpolation``).  Returns ``y [B, F, T, 2A]``,
+    ``h_hat [B, U, F, T, 2A]`` (FOCC pair average, then per-PRB nearest-pilot gather)
+    and ``pe [U, F, T, 2]``.
+    """
+    y = np.concatenate([y_real, y_imag], axis=-1)
+    h = np.concatenate([h_ls_real, h_ls_imag], axis=-1)           # [B, Npil, U, 2A]
+    h = np.transpose(h, (0, 3, 2, 1))                              # [B, 2A, U, Npil]
+    h = focc_removal(h)
+    B, F, T = y.shape[0], y.shape[1], y.shape[2]
+    nsym = dmrs_ofdm_pos.shape[-1]
+    nsc = dmrs_subcarrier_pos.shape[-1]
+    nprb = h.shape[-1] // (nsc * nsym)
+    assert nprb * 12 == F
+    # [B, 2A, U, nsym, nprb, nsc] -> [B, 2A, U, nprb, nsym * nsc]
+    hp = h.reshape(B, h.shape[1], h.shape[2], nsym, nprb, nsc).transpose(0, 1, 2, 4, 3, 5)
+    hp = hp.reshape(B, h.shape[1], h.shape[2], nprb, nsym * nsc)
+    nn, pe = aerial_nn_indices(dmrs_ofdm_pos, dmrs_subcarrier_pos, T, nprb)
+    out = np.zeros((B, num_tx, F, T, h.shape[1]), h.dtype)
+    for u in range(num_tx):
+        idx = nn[u, 0]                                             # [T, 12]
+        g = hp[:, :, u][:, :, :, idx]                              # [B, 2A, nprb, T, 12]
+        g = g.transpose(0, 2, 4, 3, 1).reshape(B, F, T, h.shape[1])
+        out[:, u] = g
+    return y, out, pe[:num_tx]
+
+
+def aerial_ls_pilots(y_complex_bfta, x_pilot_bupf, cdm_groups, dmrs_symbols, num_prbs):
+    """Test helper: LS estimates at each user's DMRS REs in the Aerial pilot order
+    ``[B, Npil, U, A]`` (real, imag), Npil = nsym * nprb * 6.  ``y_complex_bfta``
+    [B, F, T, A], ``x_pilot_bupf`` [B, U, F, T] transmitted symbols."""
+    B, F, T, A = y_complex_bfta.shape
+    U = len(cdm_groups)
+    nsym = len(dmrs_symbols)
+    out = np.zeros((B, nsym * num_prbs * 6, U, A), np.complex128)
+    for u, g in enumerate(cdm_groups):
+        for k, ts in enumerate(dmrs_symbols):
+            for prb in range(num_prbs):
+                for j in range(6):
+                    f = prb * 12 + g + 2 * j
+                    x = x_pilot_bupf[:, u, f, ts]
+                    safe = np.where(np.abs(x) > 0, x, 1.0)
+                    ls = np.where(np.abs(x)[:, None] > 0, y_complex_bfta[:, f, ts, :] / safe[:, None], 0)
+                    out[:, (k * num_prbs + prb) * 6 + j, u, :] = ls
+    return out.real.astype(np.float32), out.imag.astype(np.float32)

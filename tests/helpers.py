@@ -97,3 +97,43 @@ def compare(ref, got):
            for r, g in zip(ref["llr"], got["llr"])]
     out["llr_rms_rel"] = max(rms)
     return out
+
+
+@dataclasses.dataclass
+class AerialCase:
+    """NeuralReceiverONNX inputs (Aerial pilot order) + the oracle's preprocessed CGNN case."""
+    inputs: dict
+    case: Case
+
+
+def make_aerial_case(config="nrx_rt", batch=2, users=2, prbs=4, snr_db=15.0, seed=1, active=None):
+    base = make_case(config, batch=batch, users=users, prbs=prbs, snr_db=snr_db, seed=seed, active=active)
+    cfg = base.cfg
+    groups = user_cdm_groups(cfg, users)
+    syms = list(dmrs_symbols(cfg))
+    sl = base.slots
+    yc = np.transpose(sl.y_complex[:, 0], (0, 3, 2, 1))                 # [B, F, T, A]
+    h_re, h_im = pe_ref.aerial_ls_pilots(yc, sl.x, groups, syms, prbs)
+    ofdm = np.array([syms for _ in range(users)], np.int32)
+    scp = np.array([[g + 2 * j for j in range(6)] for g in groups], np.int32)
+    inputs = dict(y_real=np.ascontiguousarray(yc.real, np.float32), y_imag=np.ascontiguousarray(yc.imag, np.float32),
+                  h_ls_real=h_re, h_ls_imag=h_im, dmrs_port_mask=base.active.copy(),
+                  dmrs_ofdm_pos=ofdm, dmrs_subcarrier_pos=scp)
+    y, h, pe = pe_ref.aerial_preprocess(inputs["y_real"], inputs["y_imag"], h_re, h_im, ofdm, scp, users)
+    mask = np.zeros((batch, users, base.spec.num_mcs), np.float32)
+    mask[..., 0] = 1.0                    # single MCS (the ONNX export's dummy mask)
+    case = dataclasses.replace(base, y=y, h_hat=h, pe=pe, mcs_mask=mask)
+    return AerialCase(inputs, case)
+
+
+def run_engine_aerial(ac: AerialCase, precision="f16", engine=None):
+    import torch
+    from neural_rx_amd.receiver import CGNNEngine
+    eng = engine or CGNNEngine(ac.case.spec, ac.case.weights)
+    dev = "cuda:0"
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in ac.inputs.items()}
+    llr, h = eng.forward_aerial(t["y_real"], t["y_imag"], t["h_ls_real"], t["h_ls_imag"], t["dmrs_port_mask"],
+                                t["dmrs_ofdm_pos"], t["dmrs_subcarrier_pos"], num_it=ac.case.num_it,
+                                precision=precision)
+    torch.cuda.synchronize()
+    return llr.cpu().numpy(), h.cpu().numpy()
