@@ -178,6 +178,7 @@ def main():
     latency = None
     if not args.no_latency and rank == 0:
         latency = measure_latency(torch, eng, spec, cfg, args, groups, dev, num_it)
+        latency["132prb_aerial_contract"] = measure_latency_aerial(torch, eng, spec, cfg, args, groups, dev, num_it)
 
     # ---- CPU baseline: the numpy oracle (fp32) on a bounded sample of the same workload
     cpu = None
@@ -267,6 +268,65 @@ def measure_latency(torch, eng, spec, cfg, args, groups, dev, num_it):
                     "e2e_p99": round(float(np.percentile(e2e, 99)), 4),
                     "batch1_slots_per_s_e2e": round(1e3 / float(np.median(e2e)), 1)}
     return res
+
+
+def measure_latency_aerial(torch, eng, spec, cfg, args, groups, dev, num_it, prbs=132):
+    """Batch-1 latency of the Aerial / TensorRT contract (NeuralReceiverONNX I/O: raw rx
+    grid + LS pilots in, Aerial-layout LLRs + refined h_hat out; FOCC, NN interpolation and
+    PE on the GPU) at the reference TRT engine's shape (nrx_rt, 2 UE, 132 PRB).  e2e = H2D of
+    every input + compute + D2H of both outputs, as trtexec's 1.409 ms median includes."""
+    from neural_rx_amd import synth
+    from neural_rx_amd.config import dmrs_symbols
+    U = args.users
+    syms = list(dmrs_symbols(cfg))
+    s = synth.generate(1, U, prbs, spec.num_rx_ant, [spec.bits[0]] * U, groups, syms, snr_db=10.0, seed=78)
+    yc = np.transpose(s.y_complex[:, 0], (0, 3, 2, 1))
+    h_re, h_im = synth.aerial_ls_pilots(yc, s.x, groups, syms, prbs)
+    host = {"y_real": np.ascontiguousarray(yc.real, np.float32), "y_imag": np.ascontiguousarray(yc.imag, np.float32),
+            "h_ls_real": h_re, "h_ls_imag": h_im, "dmrs_port_mask": s.active}
+    hp = {k: torch.from_numpy(np.ascontiguousarray(v)).pin_memory() for k, v in host.items()}
+    d = {k: v.to(dev) for k, v in hp.items()}
+    ofdm = torch.tensor([syms] * U, dtype=torch.int32, device=dev)
+    scp = torch.tensor([[g + 2 * j for j in range(6)] for g in groups], dtype=torch.int32, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+    call = lambda: eng.forward_aerial(d["y_real"], d["y_imag"], d["h_ls_real"], d["h_ls_imag"], d["dmrs_port_mask"],
+                                      ofdm, scp, num_it, args.precision)
+    with torch.cuda.stream(stream):
+        for _ in range(3):
+            call()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=stream):
+        llr, h = call()
+    torch.cuda.synchronize()
+    host_llr = torch.empty(llr.shape, dtype=torch.float32).pin_memory()
+    host_h = torch.empty(h.shape, dtype=torch.float32).pin_memory()
+    n = args.latency_iters
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    with torch.cuda.stream(stream):
+        for i in range(n):
+            ev[i][0].record(stream)
+            g.replay()
+            ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    dev_ms = np.array([a_.elapsed_time(b_) for a_, b_ in ev])
+    e2e = []
+    with torch.cuda.stream(stream):
+        for i in range(n):
+            t0 = time.perf_counter()
+            for k in d:
+                d[k].copy_(hp[k], non_blocking=True)
+            g.replay()
+            host_llr.copy_(llr, non_blocking=True)
+            host_h.copy_(h, non_blocking=True)
+            stream.synchronize()
+            e2e.append(time.perf_counter() - t0)
+    e2e = np.array(e2e) * 1e3
+    return {"shape": f"llr {tuple(llr.shape)}, h_hat {tuple(h.shape)}",
+            "device_p50": round(float(np.median(dev_ms)), 4),
+            "e2e_p50": round(float(np.median(e2e)), 4),
+            "e2e_p99": round(float(np.percentile(e2e, 99)), 4),
+            "batch1_slots_per_s_e2e": round(1e3 / float(np.median(e2e)), 1)}
 
 
 def cpu_baseline(spec, cfg, slots, pe_np, args, num_it):

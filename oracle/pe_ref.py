@@ -136,22 +136,3 @@ def aerial_preprocess(y_real, y_imag, h_ls_real, h_ls_imag, dmrs_ofdm_pos, dmrs_
         out[:, u] = g
     return y, out, pe[:num_tx]
 
-
-def aerial_ls_pilots(y_complex_bfta, x_pilot_bupf, cdm_groups, dmrs_symbols, num_prbs):
-    """Test helper: LS estimates at each user's DMRS REs in the Aerial pilot order
-    ``[B, Npil, U, A]`` (real, imag), Npil = nsym * nprb * 6.  ``y_complex_bfta``
-    [B, F, T, A], ``x_pilot_bupf`` [B, U, F, T] transmitted symbols."""
-    B, F, T, A = y_complex_bfta.shape
-    U = len(cdm_groups)
-    nsym = len(dmrs_symbols)
-    out = np.zeros((B, nsym * num_prbs * 6, U, A), np.complex128)
-    for u, g in enumerate(cdm_groups):
-        for k, ts in enumerate(dmrs_symbols):
-            for prb in range(num_prbs):
-                for j in range(6):
-                    f = prb * 12 + g + 2 * j
-                    x = x_pilot_bupf[:, u, f, ts]
-                    safe = np.where(np.abs(x) > 0, x, 1.0)
-                    ls = np.where(np.abs(x)[:, None] > 0, y_complex_bfta[:, f, ts, :] / safe[:, None], 0)
-                    out[:, (k * num_prbs + prb) * 6 + j, u, :] = ls
-    return out.real.astype(np.float32), out.imag.astype(np.float32)

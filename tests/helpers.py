@@ -113,7 +113,7 @@ def make_aerial_case(config="nrx_rt", batch=2, users=2, prbs=4, snr_db=15.0, see
     syms = list(dmrs_symbols(cfg))
     sl = base.slots
     yc = np.transpose(sl.y_complex[:, 0], (0, 3, 2, 1))                 # [B, F, T, A]
-    h_re, h_im = pe_ref.aerial_ls_pilots(yc, sl.x, groups, syms, prbs)
+    h_re, h_im = synth.aerial_ls_pilots(yc, sl.x, groups, syms, prbs)
     ofdm = np.array([syms for _ in range(users)], np.int32)
     scp = np.array([[g + 2 * j for j in range(6)] for g in groups], np.int32)
     inputs = dict(y_real=np.ascontiguousarray(yc.real, np.float32), y_imag=np.ascontiguousarray(yc.imag, np.float32),
