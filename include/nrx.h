@@ -160,6 +160,16 @@ int nrx_aerial_workspace_size(const nrx_handle* h, const nrx_aerial_io* io, size
 int nrx_forward_aerial(nrx_handle* h, const nrx_aerial_io* io, void* workspace, size_t workspace_bytes,
                        void* stream);
 
+/* Coded-bit layout of one LLR head (Sionna sign): out[B][U][n_data * bits] with
+ * out[b][u][i * bits + k] = llr[b][u][f][t][k] for the i-th data RE, data_re[i] = t * F + f
+ * in resource-grid order (symbol-major) -- the ResourceGridDemapper + flatten of
+ * CGNNOFDM.forward (neural_rx.py:843-852) and DataEvaluator.post_process_llrs
+ * (onnx_utils.py:473-516).  `llr` points at head h of the nrx_forward output
+ * ([B][U][F][T][bits_stride]); data_re is a device array.  Asynchronous on `stream`. */
+int nrx_llr_demap(const float* llr, int32_t batch, int32_t num_tx, int32_t num_subcarriers,
+                  int32_t num_symbols, int32_t bits_stride, int32_t bits, const int32_t* data_re,
+                  int32_t n_data, float* out, void* stream);
+
 /* Host helper: nearest-pilot positional encoding pe[U][F][T][2] for DMRS
  * configuration type 1 (restates onnx_utils.py:172-260 for the product path).
  * dmrs_symbols: the DMRS OFDM symbol indices; cdm_group[u] in {0,1}. */

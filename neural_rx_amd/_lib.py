@@ -23,6 +23,7 @@ EXPORTS = [
     "nrx_create", "nrx_weight_layout", "nrx_workspace_size", "nrx_forward", "nrx_destroy",
     "nrx_compute_pe", "nrx_flops_per_re_user", "nrx_last_error", "nrx_api_version",
     "nrx_profile_enable", "nrx_profile_read", "nrx_aerial_workspace_size", "nrx_forward_aerial",
+    "nrx_llr_demap",
 ]
 KERNELS = ["norm", "state_init", "state_update"]
 
@@ -147,6 +148,9 @@ def load(path: str = LIB_PATH):
     lib.nrx_aerial_workspace_size.restype = c.c_int
     lib.nrx_forward_aerial.argtypes = [c.c_void_p, P(nrx_aerial_io), c.c_void_p, c.c_size_t, c.c_void_p]
     lib.nrx_forward_aerial.restype = c.c_int
+    lib.nrx_llr_demap.argtypes = [c.c_void_p, c.c_int32, c.c_int32, c.c_int32, c.c_int32, c.c_int32, c.c_int32,
+                                  c.c_void_p, c.c_int32, c.c_void_p, c.c_void_p]
+    lib.nrx_llr_demap.restype = c.c_int
     lib.nrx_api_version.argtypes = []
     lib.nrx_api_version.restype = c.c_int32
     _lib = lib

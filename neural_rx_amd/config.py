@@ -15,6 +15,8 @@ import configparser
 import dataclasses
 from typing import List, Optional, Tuple
 
+import numpy as np
+
 # 5G NR MCS table 1 (TS 38.214 Table 5.1.3.1-1): modulation order per MCS index.
 # Only the order matters for the NRX (num_bits_per_symbol per head).
 _MCS_TABLE1_QM = [2] * 10 + [4] * 7 + [6] * 12  # MCS 0..28
@@ -252,3 +254,14 @@ def user_cdm_groups(cfg: NRXConfig, num_users: int) -> Tuple[int, ...]:
         else:
             groups.append(u % 2)
     return tuple(groups)
+
+
+def data_re_indices(cfg: NRXConfig, num_subcarriers: int, num_symbols: int = 14) -> np.ndarray:
+    """Data-carrying REs of the PUSCH resource grid as ``t * F + f`` in grid order
+    (symbol-major), int32.  DMRS type 1 with two CDM groups without data: the DMRS symbols
+    carry no data (jumpstart_tutorial.ipynb:339); no guard / DC subcarriers in a PUSCH
+    allocation.  The reference's RG type grid (siona_tf.py:2153-2195) marks the same REs
+    0 = data; ``argsort`` of it (onnx_utils.py:465) lists them in this order."""
+    dm = set(dmrs_symbols(cfg))
+    ts = [t for t in range(num_symbols) if t not in dm]
+    return np.array([t * num_subcarriers + f for t in ts for f in range(num_subcarriers)], np.int32)

@@ -8,8 +8,9 @@
 //                     gathered per PRB by the NN index     (_focc_removal, _nn_interpolation)
 //   k_aerial_llr      llr[B][U][F][T][bits] -> Aerial [B][bits][U][F][T], negated
 //                     (Sionna LLR = log p1/p0, Aerial = log p0/p1; neural_rx.py:1808-1811)
+//   k_llr_demap       grid LLRs -> per-user coded-bit vector of the data REs
 //
-// All three are gathers / transposes over a few MB: HBM-bound, one pass, coalesced along
+// All four are gathers / transposes over a few MB: HBM-bound, one pass, coalesced along
 // the fastest output axis.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -148,6 +149,33 @@ __global__ __launch_bounds__(256) void k_aerial_llr(const float* __restrict__ ll
   const int uft = idx % (U * F * T);
   const int k = idx / (U * F * T);
   out[(size_t)b * n + idx] = -llr[((size_t)b * U * F * T + uft) * bits_max + k];
+}
+
+// Coded-bit layout: out[b][u][i * bits + k] = llr[b][u][f][t][k] for the
+// i-th data RE (t * F + f = data_re[i], symbol-major as Sionna's ResourceGridDemapper and
+// DataEvaluator.post_process_llrs gather it: CGNNOFDM.forward neural_rx.py:843-852,
+// onnx_utils.py:473-516); one thread per output element.
+__global__ __launch_bounds__(256) void k_llr_demap(const float* __restrict__ llr, int F, int T, int bits_stride,
+                                                    int bits, const int32_t* __restrict__ data_re, int n_data,
+                                                    size_t total, float* __restrict__ out) {
+  const size_t n = (size_t)n_data * bits;   // per (b, u)
+  for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (size_t)gridDim.x * 256) {
+    const size_t bu = idx / n;
+    const int r = (int)(idx - bu * n);
+    const int i = r / bits, k = r % bits;
+    const int re = data_re[i];
+    const int t = re / F, f = re % F;
+    out[idx] = llr[((bu * F + f) * T + t) * bits_stride + k];
+  }
+}
+
+hipError_t launch_llr_demap(const float* llr, int B, int U, int F, int T, int bits_stride, int bits,
+                            const int32_t* data_re, int n_data, float* out, hipStream_t st) {
+  const size_t total = (size_t)B * U * n_data * bits;
+  size_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  k_llr_demap<<<(unsigned)blocks, 256, 0, st>>>(llr, F, T, bits_stride, bits, data_re, n_data, total, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_aerial_tables(const int32_t* ofdm_pos, const int32_t* sc_pos, int U, int nsym, int npil, int T,

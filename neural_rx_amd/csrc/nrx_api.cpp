@@ -584,6 +584,19 @@ int nrx_forward_aerial(nrx_handle* h, const nrx_aerial_io* io, void* workspace, 
   return NRX_OK;
 }
 
+int nrx_llr_demap(const float* llr, int32_t batch, int32_t num_tx, int32_t num_subcarriers, int32_t num_symbols,
+                  int32_t bits_stride, int32_t bits, const int32_t* data_re, int32_t n_data, float* out,
+                  void* stream) {
+  if (!llr || !data_re || !out) return fail(NRX_ERR_INVALID_ARG, "null tensor pointer");
+  if (batch < 1 || num_tx < 1 || num_subcarriers < 1 || num_symbols < 1 || bits < 1 || bits > bits_stride ||
+      n_data < 1 || n_data > num_subcarriers * num_symbols)
+    return fail(NRX_ERR_SHAPE, "inconsistent demap shape");
+  hipError_t e = launch_llr_demap(llr, batch, num_tx, num_subcarriers, num_symbols, bits_stride, bits, data_re,
+                                  n_data, out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "llr demap launch");
+  return NRX_OK;
+}
+
 int nrx_profile_enable(nrx_handle* h, int32_t enable) {
   if (!h) return fail(NRX_ERR_INVALID_ARG, "null handle");
   if (enable) {

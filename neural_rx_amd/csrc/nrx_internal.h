@@ -93,4 +93,7 @@ hipError_t launch_aerial_inputs(const float* y_re, const float* y_im, const floa
 hipError_t launch_aerial_llr(const float* llr, int B, int U, int F, int T, int bits_max, int bits, float* out,
                              hipStream_t st);
 
+hipError_t launch_llr_demap(const float* llr, int B, int U, int F, int T, int bits_stride, int bits,
+                            const int32_t* data_re, int n_data, float* out, hipStream_t st);
+
 }  // namespace nrx

@@ -24,7 +24,8 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from . import _lib
-from .config import ModelSpec, NRXConfig, dmrs_symbols, get_config, spec_from_config, user_cdm_groups
+from .config import (ModelSpec, NRXConfig, data_re_indices, dmrs_symbols, get_config, spec_from_config,
+                     user_cdm_groups)
 from . import weights as _weights
 
 NUM_SYMBOLS = 14
@@ -176,6 +177,22 @@ class CGNNEngine:
         return llr, h_ref
 
 
+    # -------------------------------------------------------------- coded-bit layout
+    def llr_demap(self, llr_head, bits, data_re, stream=None):
+        """``llr_head [B,U,F,T,bits_stride]`` (one head of ``forward``'s output, Sionna sign)
+        -> ``[B,U,n_data*bits]``: the data REs in resource-grid order (include/nrx.h
+        nrx_llr_demap; ResourceGridDemapper + flatten of CGNNOFDM.forward, neural_rx.py:843-852)."""
+        torch = _torch()
+        if not llr_head.is_contiguous():
+            raise ValueError("llr_head must be contiguous (a head slice of the forward output)")
+        B, U, F, T, stride = llr_head.shape
+        out = torch.empty((B, U, data_re.numel() * bits), dtype=torch.float32, device=llr_head.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(llr_head.device).cuda_stream
+        _lib.check(self._lib.nrx_llr_demap(llr_head.data_ptr(), B, U, F, T, stride, bits, data_re.data_ptr(),
+                                           data_re.numel(), out.data_ptr(), stream))
+        return out
+
     # -------------------------------------------------------------- Aerial contract
     def forward_aerial(self, y_real, y_imag, h_ls_real, h_ls_imag, dmrs_port_mask, dmrs_ofdm_pos,
                        dmrs_subcarrier_pos, num_it=None, precision="f16", want_h=True, stream=None):
@@ -299,6 +316,7 @@ class CGNN:
         y, pe, h_hat, active_tx, mcs_ue_mask = inputs
         llr, h = self.engine.forward(y, pe, h_hat, active_tx, mcs_ue_mask, self._num_it,
                                      self.precision)
+        self.last_raw_llr = llr          # [H, B, U, F, T, bits_max] (for coded-bit demapping)
         sp = self.spec
         per_mcs = []
         for m, nb in enumerate(sp.bits):
@@ -339,8 +357,17 @@ class NeuralReceiver:
             self._pe_cache[key] = torch.from_numpy(pe).to(f"cuda:{self.device}")
         return self._pe_cache[key]
 
+    def data_re(self, num_subcarriers: int):
+        """Device int32 table of the data REs (t * F + f, resource-grid order)."""
+        torch = _torch()
+        key = ("re", num_subcarriers)
+        if key not in self._pe_cache:
+            self._pe_cache[key] = torch.from_numpy(data_re_indices(self.cfg, num_subcarriers)).to(
+                f"cuda:{self.device}")
+        return self._pe_cache[key]
+
     def __call__(self, rx_grid, pe=None, active_dmrs=None, h_hat=None, mcs_ue_mask=None,
-                 num_it=None, layout: str = "sionna", return_h_hat: bool = False):
+                 num_it=None, layout: str = "sionna", return_h_hat: bool = False, demap: bool = False):
         torch = _torch()
         if num_it is not None:
             self.num_it = num_it
@@ -364,8 +391,14 @@ class NeuralReceiver:
         if pe is None:
             pe = self.positional_encoding(U, F)
         llrs, h_hats = self.cgnn([y, pe, h_hat, active, mcs_ue_mask])
-        llr = llrs[-1][0] if self.spec.num_mcs == 1 else llrs[-1]
         h_ref = h_hats[-1]
+        if demap:
+            # CGNNOFDM.forward's output (neural_rx.py:843-858): per-user coded bits of the
+            # data REs, [B, U, num_coded_bits] for MCS 0 (mcs_arr_eval[0])
+            raw = self.cgnn.last_raw_llr
+            llr = self.cgnn.engine.llr_demap(raw[0], self.spec.bits[0], self.data_re(F))
+            return (llr, h_ref) if return_h_hat else llr
+        llr = llrs[-1][0] if self.spec.num_mcs == 1 else llrs[-1]
         if layout == "aerial":
             llr = -llr.permute(0, 4, 1, 2, 3)   # [B,bits,U,F,T], LLR = log p0/p1
         return (llr, h_ref) if return_h_hat else llr

@@ -130,3 +130,53 @@ def test_aerial_receiver_trt_shapes():
     assert tuple(llr.shape) == (1, 4, 2, 1584, 14)
     assert tuple(h.shape) == (1, 2, 1584, 14, 8)
     assert torch.isfinite(llr).all() and torch.isfinite(h).all()
+
+
+# ------------------------------------------------------------------ coded-bit layout (f2)
+def test_data_re_count_matches_reference_kat():
+    # 4 PRB, 16-QAM, DMRS on 2 symbols without data: 2304 coded bits per user
+    # (jumpstart_tutorial.ipynb:312)
+    from neural_rx_amd.config import data_re_indices, get_config
+    re = data_re_indices(get_config("nrx_rt"), 48)
+    assert re.size * 4 == 2304
+    # grid order = argsort of the RG type grid (data = 0 first, stable, symbol-major)
+    typ = np.ones((14, 48), np.int32)
+    typ[[t for t in range(14) if t not in (2, 11)]] = 0
+    np.testing.assert_array_equal(np.argsort(typ.ravel(), kind="stable")[:re.size], re)
+
+
+@pytest.mark.gpu
+def test_llr_demap_matches_numpy_gather():
+    import torch
+    from neural_rx_amd.config import data_re_indices, get_config
+    from neural_rx_amd.receiver import NeuralReceiver
+    case_rng = np.random.default_rng(5)
+    B, U, F, T, S = 3, 2, 48, 14, 6
+    llr = case_rng.standard_normal((B, U, F, T, S)).astype(np.float32)
+    re = data_re_indices(get_config("nrx_rt"), F)
+    nrx = NeuralReceiver("nrx_rt")
+    out = nrx.cgnn.engine.llr_demap(torch.from_numpy(llr).cuda(), 4, torch.from_numpy(re).cuda())
+    torch.cuda.synchronize()
+    t, f = re // F, re % F
+    ref = llr[:, :, f, t, :4].reshape(B, U, -1)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+def test_receiver_demap_output_is_coded_bits():
+    import torch
+    from neural_rx_amd import synth
+    from neural_rx_amd.receiver import NeuralReceiver
+    from tests.helpers import make_case
+    case = make_case("nrx_rt", batch=2, users=2, prbs=4, snr_db=20.0, seed=8)
+    nrx = NeuralReceiver("nrx_rt", precision="f32x")
+    yc = torch.from_numpy(case.slots.y_complex).cuda()
+    llr = nrx(yc, active_dmrs=torch.from_numpy(case.active).cuda(),
+              h_hat=torch.from_numpy(case.h_hat).cuda(), demap=True)
+    torch.cuda.synchronize()
+    assert tuple(llr.shape) == (2, 2, 2304)
+    # coded bits in grid order: the transmitted bits of the data REs, symbol-major
+    dm = case.slots.data_mask
+    bits = case.slots.bits[:, :, :, dm, :4].transpose(0, 1, 3, 2, 4).reshape(2, 2, -1)
+    ber = float(((llr.cpu().numpy() > 0).astype(np.uint8) != bits).mean())
+    assert ber < 0.01
