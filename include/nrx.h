@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NRX_API_VERSION 2
+#define NRX_API_VERSION 3
 
 enum nrx_status {
   NRX_OK = 0,
@@ -169,6 +169,81 @@ int nrx_forward_aerial(nrx_handle* h, const nrx_aerial_io* io, void* workspace, 
 int nrx_llr_demap(const float* llr, int32_t batch, int32_t num_tx, int32_t num_subcarriers,
                   int32_t num_symbols, int32_t bits_stride, int32_t bits, const int32_t* data_re,
                   int32_t n_data, float* out, void* stream);
+
+/* ---------------------------------------------------------------- slot generator
+ * Seeded synthetic PUSCH slots generated on the GPU -- replaces the
+ * transmitter + channel + LS-estimator chain of E2E_Model.forward (utils/e2e_model.py:
+ * 219-344: random active DMRS ports 187-193, x *= active 311-313, Eb/N0 -> no 323-332)
+ * for evaluation loops that never leave the device.  The algorithm (Philox4x32-10 draws
+ * keyed by seed and counted by the global slot index slot_offset + b, Gray QAM / DMRS type
+ * 1 QPSK x sqrt(2), tapped-delay-line channel with exponential PDP and sum-of-sinusoids
+ * Doppler, AWGN, LS at the nearest own pilot) is stated in oracle/synth_ref.py. */
+typedef struct nrx_gen_desc {
+  int32_t batch;               /* B slots in this call */
+  int32_t num_tx;              /* U DMRS ports, 1..16 */
+  int32_t num_subcarriers;     /* F */
+  int32_t num_symbols;         /* T, must be 14 */
+  int32_t num_rx_ant;          /* A, 1..16 */
+  int32_t num_dmrs_symbols;    /* 1..4 */
+  int32_t dmrs_symbols[4];     /* ascending */
+  int32_t dmrs_symbol_mask;    /* bit t set <=> t is a DMRS symbol (no data) */
+  int32_t cdm_group[16];       /* per port, 0/1 (DMRS type 1: even / odd subcarriers) */
+  int32_t num_mcs;             /* M, 1..8 */
+  int32_t mcs_bits[8];         /* bits per symbol of each MCS: 2, 4 or 6 */
+  int32_t mcs_of_user[16];     /* MCS index per port, -1 = drawn per slot */
+  int32_t num_active;          /* active ports per slot (1..U), placed at random */
+  int32_t num_taps;            /* TDL taps, 1..8 */
+  int32_t num_sinusoids;       /* Doppler sinusoids per tap, 1..16 */
+  int32_t pad_;
+  double max_delay_s;
+  double max_doppler_hz;
+  double subcarrier_spacing;   /* Hz */
+  double no;                   /* noise variance per RE (complex) */
+  uint64_t seed;
+  int64_t slot_offset;         /* global index of slot 0 of this call */
+} nrx_gen_desc;
+
+/* Device outputs; any pointer except y may be NULL. */
+typedef struct nrx_gen_out {
+  float* y;                    /* [B][F][T][2A] (nrx_io.y layout) */
+  float* h_hat;                /* [B][U][F][T][2A] LS + nearest-neighbour */
+  float* h;                    /* [B][U][F][T][2A] true channel */
+  float* active;               /* [B][U] */
+  float* mcs_mask;             /* [B][U][M] one-hot (nrx_io.mcs_mask) */
+  uint8_t* mcs;                /* [B][U] MCS index */
+  uint8_t* bits;               /* [B][U][F][T][bits_stride], 0 on DMRS REs and k >= bits */
+  int32_t bits_stride;         /* >= max(mcs_bits) */
+  int32_t pad_;
+  float* y_real;               /* [B][F][T][A] Aerial rx_slot_real */
+  float* y_imag;
+  float* h_ls_real;            /* [B][Npil][U][A] Aerial LS pilots (nrx_aerial_io), needs F % 12 == 0 */
+  float* h_ls_imag;
+} nrx_gen_out;
+
+int nrx_gen_workspace_size(const nrx_gen_desc* desc, size_t* bytes);
+int nrx_generate_slots(const nrx_gen_desc* desc, const nrx_gen_out* out, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
+/* Uncoded error counters of one batch (sim_ber's counting, scripts/evaluate.py:193-202,
+ * with the active-port masking of E2E_Model._mask_active_dmrs, e2e_model.py:195-209):
+ * counts[u][0..3] += (bit errors, bits, block errors, blocks) over the active (slot, user)
+ * pairs, data REs and the first mcs_bits[mcs[b][u]] bits; hard decision LLR > 0 -> 1; a
+ * block is one (slot, user) grid.  Asynchronous on `stream`. */
+typedef struct nrx_count_io {
+  int32_t batch, num_tx, num_subcarriers, num_symbols;
+  int32_t num_heads;           /* H heads in llr; head = mcs if H > 1 else 0 */
+  int32_t bits_stride;         /* last dim of llr and bits */
+  int32_t num_mcs;
+  int32_t mcs_bits[8];
+  int32_t dmrs_symbol_mask;
+  const float* llr;            /* [H][B][U][F][T][bits_stride] (nrx_io.llr) */
+  const uint8_t* bits;         /* [B][U][F][T][bits_stride] */
+  const uint8_t* mcs;          /* [B][U] or NULL (= 0) */
+  const float* active;         /* [B][U] */
+  int64_t* counts;             /* [U][4] accumulated (device) */
+} nrx_count_io;
+
+int nrx_count_errors(const nrx_count_io* io, void* stream);
 
 /* Host helper: nearest-pilot positional encoding pe[U][F][T][2] for DMRS
  * configuration type 1 (restates onnx_utils.py:172-260 for the product path).

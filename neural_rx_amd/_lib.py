@@ -10,7 +10,8 @@ import ctypes
 import os
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libnrx.so")
+# NRX_LIB_PATH: diagnostic override (kernel-variant A/B runs); the default is the in-tree build
+LIB_PATH = os.environ.get("NRX_LIB_PATH") or os.path.join(LIB_DIR, "libnrx.so")
 
 NRX_OK = 0
 NRX_PREC_F16 = 0
@@ -23,7 +24,7 @@ EXPORTS = [
     "nrx_create", "nrx_weight_layout", "nrx_workspace_size", "nrx_forward", "nrx_destroy",
     "nrx_compute_pe", "nrx_flops_per_re_user", "nrx_last_error", "nrx_api_version",
     "nrx_profile_enable", "nrx_profile_read", "nrx_aerial_workspace_size", "nrx_forward_aerial",
-    "nrx_llr_demap",
+    "nrx_llr_demap", "nrx_gen_workspace_size", "nrx_generate_slots", "nrx_count_errors",
 ]
 KERNELS = ["norm", "state_init", "state_update"]
 
@@ -97,6 +98,70 @@ class nrx_aerial_io(ctypes.Structure):
     ]
 
 
+class nrx_gen_desc(ctypes.Structure):
+    _fields_ = [
+        ("batch", ctypes.c_int32),
+        ("num_tx", ctypes.c_int32),
+        ("num_subcarriers", ctypes.c_int32),
+        ("num_symbols", ctypes.c_int32),
+        ("num_rx_ant", ctypes.c_int32),
+        ("num_dmrs_symbols", ctypes.c_int32),
+        ("dmrs_symbols", ctypes.c_int32 * 4),
+        ("dmrs_symbol_mask", ctypes.c_int32),
+        ("cdm_group", ctypes.c_int32 * 16),
+        ("num_mcs", ctypes.c_int32),
+        ("mcs_bits", ctypes.c_int32 * 8),
+        ("mcs_of_user", ctypes.c_int32 * 16),
+        ("num_active", ctypes.c_int32),
+        ("num_taps", ctypes.c_int32),
+        ("num_sinusoids", ctypes.c_int32),
+        ("pad_", ctypes.c_int32),
+        ("max_delay_s", ctypes.c_double),
+        ("max_doppler_hz", ctypes.c_double),
+        ("subcarrier_spacing", ctypes.c_double),
+        ("no", ctypes.c_double),
+        ("seed", ctypes.c_uint64),
+        ("slot_offset", ctypes.c_int64),
+    ]
+
+
+class nrx_gen_out(ctypes.Structure):
+    _fields_ = [
+        ("y", ctypes.c_void_p),
+        ("h_hat", ctypes.c_void_p),
+        ("h", ctypes.c_void_p),
+        ("active", ctypes.c_void_p),
+        ("mcs_mask", ctypes.c_void_p),
+        ("mcs", ctypes.c_void_p),
+        ("bits", ctypes.c_void_p),
+        ("bits_stride", ctypes.c_int32),
+        ("pad_", ctypes.c_int32),
+        ("y_real", ctypes.c_void_p),
+        ("y_imag", ctypes.c_void_p),
+        ("h_ls_real", ctypes.c_void_p),
+        ("h_ls_imag", ctypes.c_void_p),
+    ]
+
+
+class nrx_count_io(ctypes.Structure):
+    _fields_ = [
+        ("batch", ctypes.c_int32),
+        ("num_tx", ctypes.c_int32),
+        ("num_subcarriers", ctypes.c_int32),
+        ("num_symbols", ctypes.c_int32),
+        ("num_heads", ctypes.c_int32),
+        ("bits_stride", ctypes.c_int32),
+        ("num_mcs", ctypes.c_int32),
+        ("mcs_bits", ctypes.c_int32 * 8),
+        ("dmrs_symbol_mask", ctypes.c_int32),
+        ("llr", ctypes.c_void_p),
+        ("bits", ctypes.c_void_p),
+        ("mcs", ctypes.c_void_p),
+        ("active", ctypes.c_void_p),
+        ("counts", ctypes.c_void_p),
+    ]
+
+
 _lib = None
 
 
@@ -151,6 +216,12 @@ def load(path: str = LIB_PATH):
     lib.nrx_llr_demap.argtypes = [c.c_void_p, c.c_int32, c.c_int32, c.c_int32, c.c_int32, c.c_int32, c.c_int32,
                                   c.c_void_p, c.c_int32, c.c_void_p, c.c_void_p]
     lib.nrx_llr_demap.restype = c.c_int
+    lib.nrx_gen_workspace_size.argtypes = [P(nrx_gen_desc), P(c.c_size_t)]
+    lib.nrx_gen_workspace_size.restype = c.c_int
+    lib.nrx_generate_slots.argtypes = [P(nrx_gen_desc), P(nrx_gen_out), c.c_void_p, c.c_size_t, c.c_void_p]
+    lib.nrx_generate_slots.restype = c.c_int
+    lib.nrx_count_errors.argtypes = [P(nrx_count_io), c.c_void_p]
+    lib.nrx_count_errors.restype = c.c_int
     lib.nrx_api_version.argtypes = []
     lib.nrx_api_version.restype = c.c_int32
     _lib = lib

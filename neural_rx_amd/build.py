@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "lib", "libnrx.so")
 SOURCES = [os.path.join(CSRC, "nrx_kernels.hip"), os.path.join(CSRC, "nrx_aerial.hip"),
-           os.path.join(CSRC, "nrx_api.cpp")]
+           os.path.join(CSRC, "nrx_synth.hip"), os.path.join(CSRC, "nrx_api.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, "nrx_internal.h"),
                   os.path.join(HERE, "..", "include", "nrx.h")]
 ARCH = os.environ.get("NRX_OFFLOAD_ARCH", "gfx950")

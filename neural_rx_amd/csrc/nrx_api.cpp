@@ -597,6 +597,80 @@ int nrx_llr_demap(const float* llr, int32_t batch, int32_t num_tx, int32_t num_s
   return NRX_OK;
 }
 
+static int check_gen(const nrx_gen_desc* d) {
+  if (!d) return fail(NRX_ERR_INVALID_ARG, "desc is NULL");
+  if (d->batch < 1 || d->batch > 65535) return fail(NRX_ERR_SHAPE, "batch must be 1..65535");
+  if (d->num_tx < 1 || d->num_tx > kMaxUsers) return fail(NRX_ERR_SHAPE, "num_tx must be 1..16");
+  if (d->num_symbols != kT) return fail(NRX_ERR_SHAPE, "num_symbols must be 14");
+  if (d->num_subcarriers < 2 || d->num_subcarriers > 3300) return fail(NRX_ERR_SHAPE, "num_subcarriers must be 2..3300");
+  if (d->num_rx_ant < 1 || d->num_rx_ant > 16) return fail(NRX_ERR_SHAPE, "num_rx_ant must be 1..16");
+  if (d->num_dmrs_symbols < 1 || d->num_dmrs_symbols > 4) return fail(NRX_ERR_SHAPE, "num_dmrs_symbols must be 1..4");
+  int mask = 0;
+  for (int k = 0; k < d->num_dmrs_symbols; ++k) {
+    const int t = d->dmrs_symbols[k];
+    if (t < 0 || t >= kT || (k && t <= d->dmrs_symbols[k - 1]))
+      return fail(NRX_ERR_INVALID_ARG, "dmrs_symbols must be ascending symbol indices");
+    mask |= 1 << t;
+  }
+  if (mask != d->dmrs_symbol_mask) return fail(NRX_ERR_INVALID_ARG, "dmrs_symbol_mask does not match dmrs_symbols");
+  if (d->num_mcs < 1 || d->num_mcs > 8) return fail(NRX_ERR_INVALID_ARG, "num_mcs must be 1..8");
+  for (int m = 0; m < d->num_mcs; ++m)
+    if (d->mcs_bits[m] != 2 && d->mcs_bits[m] != 4 && d->mcs_bits[m] != 6)
+      return fail(NRX_ERR_INVALID_ARG, "mcs_bits must be 2, 4 or 6");
+  for (int u = 0; u < d->num_tx; ++u) {
+    if (d->cdm_group[u] != 0 && d->cdm_group[u] != 1) return fail(NRX_ERR_INVALID_ARG, "cdm_group must be 0/1");
+    if (d->mcs_of_user[u] < -1 || d->mcs_of_user[u] >= d->num_mcs)
+      return fail(NRX_ERR_INVALID_ARG, "mcs_of_user must be -1..num_mcs-1");
+  }
+  if (d->num_active < 1 || d->num_active > d->num_tx) return fail(NRX_ERR_INVALID_ARG, "num_active must be 1..num_tx");
+  if (d->num_taps < 1 || d->num_taps > 8) return fail(NRX_ERR_INVALID_ARG, "num_taps must be 1..8");
+  if (d->num_sinusoids < 1 || d->num_sinusoids > 16) return fail(NRX_ERR_INVALID_ARG, "num_sinusoids must be 1..16");
+  if (!(d->max_delay_s >= 0.0) || !(d->max_doppler_hz >= 0.0) || !(d->subcarrier_spacing > 0.0) || !(d->no >= 0.0))
+    return fail(NRX_ERR_INVALID_ARG, "channel parameters must be finite and non-negative (scs > 0)");
+  if (d->slot_offset < 0) return fail(NRX_ERR_INVALID_ARG, "slot_offset must be >= 0");
+  return NRX_OK;
+}
+
+int nrx_gen_workspace_size(const nrx_gen_desc* desc, size_t* bytes) {
+  if (int rc = check_gen(desc)) return rc;
+  if (!bytes) return fail(NRX_ERR_INVALID_ARG, "bytes is NULL");
+  *bytes = gen_workspace_bytes(*desc, nullptr, nullptr);
+  return NRX_OK;
+}
+
+int nrx_generate_slots(const nrx_gen_desc* desc, const nrx_gen_out* out, void* workspace, size_t workspace_bytes,
+                       void* stream) {
+  if (int rc = check_gen(desc)) return rc;
+  if (!out || !out->y || !workspace) return fail(NRX_ERR_INVALID_ARG, "null tensor pointer");
+  int bmax = 0;
+  for (int m = 0; m < desc->num_mcs; ++m) bmax = desc->mcs_bits[m] > bmax ? desc->mcs_bits[m] : bmax;
+  if (out->bits && out->bits_stride < bmax) return fail(NRX_ERR_SHAPE, "bits_stride < max(mcs_bits)");
+  if ((out->y_real == nullptr) != (out->y_imag == nullptr) || (out->h_ls_real == nullptr) != (out->h_ls_imag == nullptr))
+    return fail(NRX_ERR_INVALID_ARG, "Aerial outputs come in (real, imag) pairs");
+  if (out->h_ls_real && desc->num_subcarriers % 12)
+    return fail(NRX_ERR_SHAPE, "Aerial pilot list needs num_subcarriers % 12 == 0");
+  const size_t need = gen_workspace_bytes(*desc, nullptr, nullptr);
+  if (workspace_bytes < need)
+    return fail(NRX_ERR_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes");
+  hipError_t e = launch_generate(*desc, *out, workspace, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "slot generator launch");
+  return NRX_OK;
+}
+
+int nrx_count_errors(const nrx_count_io* io, void* stream) {
+  if (!io) return fail(NRX_ERR_INVALID_ARG, "null argument");
+  if (!io->llr || !io->bits || !io->active || !io->counts) return fail(NRX_ERR_INVALID_ARG, "null tensor pointer");
+  if (io->batch < 1 || io->num_tx < 1 || io->num_subcarriers < 1 || io->num_symbols < 1 || io->num_symbols > 31 ||
+      io->num_heads < 1 || io->num_mcs < 1 || io->num_mcs > 8 || (io->num_heads > 1 && io->num_heads != io->num_mcs))
+    return fail(NRX_ERR_SHAPE, "inconsistent counter shape");
+  for (int m = 0; m < io->num_mcs; ++m)
+    if (io->mcs_bits[m] < 1 || io->mcs_bits[m] > io->bits_stride)
+      return fail(NRX_ERR_SHAPE, "mcs_bits must be 1..bits_stride");
+  hipError_t e = launch_count_errors(*io, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "error counter launch");
+  return NRX_OK;
+}
+
 int nrx_profile_enable(nrx_handle* h, int32_t enable) {
   if (!h) return fail(NRX_ERR_INVALID_ARG, "null handle");
   if (enable) {

@@ -12,6 +12,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "../../include/nrx.h"
+
 namespace nrx {
 
 constexpr int kT = 14;        // OFDM symbols (fixed by 5G NR slot)
@@ -92,6 +94,13 @@ hipError_t launch_aerial_inputs(const float* y_re, const float* y_im, const floa
                                 float* h, hipStream_t st);
 hipError_t launch_aerial_llr(const float* llr, int B, int U, int F, int T, int bits_max, int bits, float* out,
                              hipStream_t st);
+
+// Slot generator + error counters (nrx_synth.hip); struct types from include/nrx.h.
+// gen_workspace_bytes(d, nullptr, nullptr) = workspace size.
+struct GenWs;
+size_t gen_workspace_bytes(const nrx_gen_desc& d, GenWs* w, char* base);
+hipError_t launch_generate(const nrx_gen_desc& d, const nrx_gen_out& o, void* ws, hipStream_t st);
+hipError_t launch_count_errors(const nrx_count_io& c, hipStream_t st);
 
 hipError_t launch_llr_demap(const float* llr, int B, int U, int F, int T, int bits_stride, int bits,
                             const int32_t* data_re, int n_data, float* out, hipStream_t st);

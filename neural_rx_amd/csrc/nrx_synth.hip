@@ -1,0 +1,425 @@
+// nrx_synth.hip -- seeded PUSCH slot generator and uncoded error counters on the GPU
+// (SURVEY.md 8(f) f3): the stand-in for the reference's transmitter + channel + LS chain
+// (E2E_Model.forward, utils/e2e_model.py:219-344) and sim_ber's error counting
+// (scripts/evaluate.py:193-202), so that an evaluation loop never leaves the device.
+// The algorithm is stated once, in oracle/synth_ref.py; these kernels compute the same
+// function (f64 arithmetic, one f32 rounding at the end).
+//
+//   k_gen_params   per slot: active ports (Fisher-Yates, e2e_model.py:187-193), MCS per
+//                  user, TDL delays (sorted, first = 0) and the exponential PDP
+//   k_gen_taps     per (slot, user, antenna, tap): sum-of-sinusoids tap gain g(t), T values
+//   k_gen_tx       per (slot, user, RE): Philox bits, Gray QAM / DMRS QPSK x sqrt(2), x *= active
+//   k_gen_rx       per (slot, subcarrier): the user/tap phasors of that subcarrier in LDS,
+//                  then y[a][t] = sum_u H_u x_u + AWGN (and the true channel, optional)
+//   k_gen_ls       per (slot, user, RE, antenna): LS at the nearest own pilot (closed form
+//                  of the Manhattan argmin), and the Aerial pilot list (optional)
+//   k_count_errors per (slot, user): hard decisions of the LLR head vs the sent bits on the
+//                  data REs, block reduction, 4 int64 atomics
+//
+// Random draws: Philox4x32-10 with key = seed and counter = (element, slot lo, slot hi,
+// stream), slot = slot_offset + b -- a pure function of the global slot index, so any split
+// of slots over launches or ranks generates the same slots.  All HBM-bound or
+// latency-trivial next to the CGNN (a few bytes per RE); one pass each, coalesced along the
+// fastest output axis.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/nrx.h"
+#include "nrx_internal.h"
+
+namespace nrx {
+
+struct GenWs {
+  double2* x;        // [B][U][F][T]
+  double2* gt;       // [B][U][A][L][T]
+  double* tau;       // [B][U][L]
+  double* spdp;      // [B][U][L]
+  uint8_t* mcs;      // [B][U]
+  float* active;     // [B][U]
+};
+
+namespace {
+
+enum { ST_RE = 0, ST_ACTIVE = 1, ST_MCS = 2, ST_DELAY = 3, ST_TAP = 4, ST_NOISE = 5 };
+
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kCP = 1.07;      // symbol time = 1.07 / scs (normal cyclic prefix)
+constexpr double kPDP = 3.0;      // PDP decay constant = max_delay / 3
+
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                     uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+  }
+  return {c0, c1, c2, c3};
+}
+
+__device__ __forceinline__ U4 draw(const nrx_gen_desc& d, int64_t b, int stream, uint32_t idx) {
+  const uint64_t g = (uint64_t)(d.slot_offset + b);
+  return philox(idx, (uint32_t)g, (uint32_t)(g >> 32), (uint32_t)stream, (uint32_t)d.seed,
+                (uint32_t)(d.seed >> 32));
+}
+
+__device__ __forceinline__ double uni(uint32_t w) { return ((double)w + 0.5) * 0x1p-32; }
+
+__device__ __forceinline__ double2 box_muller(uint32_t w0, uint32_t w1) {
+  const double r = sqrt(-2.0 * log(uni(w0)));
+  const double th = 2.0 * kPi * uni(w1);
+  return make_double2(r * cos(th), r * sin(th));
+}
+
+// Gray QAM of TS 38.211 5.1 (unit energy): bit k of `w`, k < m
+__device__ __forceinline__ double2 qam(uint32_t w, int m) {
+  auto s = [&](int k) { return 1.0 - 2.0 * (double)((w >> k) & 1u); };
+  if (m == 2) return make_double2(s(0) / sqrt(2.0), s(1) / sqrt(2.0));
+  if (m == 4) return make_double2(s(0) * (2.0 - s(2)) / sqrt(10.0), s(1) * (2.0 - s(3)) / sqrt(10.0));
+  return make_double2(s(0) * (4.0 - s(2) * (2.0 - s(4))) / sqrt(42.0),
+                      s(1) * (4.0 - s(3) * (2.0 - s(5))) / sqrt(42.0));
+}
+
+__global__ __launch_bounds__(64) void k_gen_params(nrx_gen_desc d, GenWs w, float* __restrict__ active_out,
+                                                    float* __restrict__ mcs_mask, uint8_t* __restrict__ mcs_out) {
+  const int b = blockIdx.x;
+  const int U = d.num_tx, L = d.num_taps, M = d.num_mcs;
+  const int i = threadIdx.x;
+  if (i == 0) {
+    uint32_t wd[16];
+    for (int q = 0; q < 4; ++q) {
+      const U4 r = draw(d, b, ST_ACTIVE, q);
+      wd[4 * q] = r.x;
+      wd[4 * q + 1] = r.y;
+      wd[4 * q + 2] = r.z;
+      wd[4 * q + 3] = r.w;
+    }
+    int arr[kMaxUsers];
+    for (int u = 0; u < U; ++u) arr[u] = u < d.num_active ? 1 : 0;
+    for (int k = U - 1; k > 0; --k) {
+      const int j = (int)(wd[k] % (uint32_t)(k + 1));
+      const int t = arr[k];
+      arr[k] = arr[j];
+      arr[j] = t;
+    }
+    for (int u = 0; u < U; ++u) {
+      w.active[b * U + u] = (float)arr[u];
+      if (active_out) active_out[b * U + u] = (float)arr[u];
+    }
+  }
+  if (i < U) {
+    const int u = i;
+    int m = d.mcs_of_user[u];
+    if (m < 0) m = (int)(draw(d, b, ST_MCS, u).x % (uint32_t)M);
+    w.mcs[b * U + u] = (uint8_t)m;
+    if (mcs_out) mcs_out[b * U + u] = (uint8_t)m;
+    if (mcs_mask)
+      for (int k = 0; k < M; ++k) mcs_mask[((size_t)b * U + u) * M + k] = k == m ? 1.0f : 0.0f;
+    double tau[8];
+    for (int l = 0; l < L; ++l) tau[l] = uni(draw(d, b, ST_DELAY, u * L + l).x) * d.max_delay_s;
+    for (int l = 1; l < L; ++l) {   // insertion sort (ascending)
+      const double v = tau[l];
+      int k = l - 1;
+      while (k >= 0 && tau[k] > v) {
+        tau[k + 1] = tau[k];
+        --k;
+      }
+      tau[k + 1] = v;
+    }
+    tau[0] = 0.0;
+    double p[8], ps = 0.0;
+    for (int l = 0; l < L; ++l) {
+      p[l] = exp(-tau[l] / (d.max_delay_s / kPDP + 1e-12));
+      ps += p[l];
+    }
+    for (int l = 0; l < L; ++l) {
+      w.tau[(b * U + u) * L + l] = tau[l];
+      w.spdp[(b * U + u) * L + l] = sqrt(p[l] / ps);
+    }
+  }
+}
+
+// one thread per (b, u, a, l): g(t) = sqrt(pdp_l) sum_s g0_s exp(j 2 pi fd_s t Tsym)
+__global__ __launch_bounds__(256) void k_gen_taps(nrx_gen_desc d, GenWs w) {
+  const int U = d.num_tx, A = d.num_rx_ant, L = d.num_taps, NS = d.num_sinusoids, T = d.num_symbols;
+  const int64_t n = (int64_t)d.batch * U * A * L;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int l = (int)(i % L);
+  const int a = (int)((i / L) % A);
+  const int u = (int)((i / ((int64_t)L * A)) % U);
+  const int64_t b = i / ((int64_t)L * A * U);
+  const double tsym = kCP / d.subcarrier_spacing;
+  double2 acc[kT];
+  for (int t = 0; t < T; ++t) acc[t] = make_double2(0.0, 0.0);
+  for (int s = 0; s < NS; ++s) {
+    const U4 r = draw(d, b, ST_TAP, (uint32_t)((((u * A + a) * L + l) * NS) + s));
+    const double2 z = box_muller(r.x, r.y);
+    const double sc = 1.0 / sqrt(2.0 * NS);
+    const double g0r = z.x * sc, g0i = z.y * sc;
+    const double fd = d.max_doppler_hz * cos(2.0 * kPi * uni(r.z));
+    for (int t = 0; t < T; ++t) {
+      const double ph = 2.0 * kPi * (fd * (t * tsym));
+      const double c = cos(ph), sn = sin(ph);
+      acc[t].x += g0r * c - g0i * sn;
+      acc[t].y += g0r * sn + g0i * c;
+    }
+  }
+  const double sp = w.spdp[(b * U + u) * L + l];
+  double2* dst = w.gt + i * T;
+  for (int t = 0; t < T; ++t) dst[t] = make_double2(acc[t].x * sp, acc[t].y * sp);
+}
+
+// one thread per (b, u, f, t)
+__global__ __launch_bounds__(256) void k_gen_tx(nrx_gen_desc d, GenWs w, uint8_t* __restrict__ bits,
+                                                int bits_stride) {
+  const int U = d.num_tx, F = d.num_subcarriers, T = d.num_symbols;
+  const int64_t n = (int64_t)d.batch * U * F * T;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int t = (int)(i % T);
+  const int f = (int)((i / T) % F);
+  const int u = (int)((i / ((int64_t)T * F)) % U);
+  const int64_t b = i / ((int64_t)T * F * U);
+  const U4 r = draw(d, b, ST_RE, (uint32_t)((u * F + f) * T + t));
+  const bool dmrs = (d.dmrs_symbol_mask >> t) & 1;
+  const int m = d.mcs_bits[w.mcs[b * U + u]];
+  double2 x;
+  if (dmrs) {
+    const double2 q = qam(r.y, 2);
+    x = (f & 1) == d.cdm_group[u] ? make_double2(q.x * sqrt(2.0), q.y * sqrt(2.0)) : make_double2(0.0, 0.0);
+  } else {
+    x = qam(r.x, m);
+  }
+  const double act = w.active[b * U + u];
+  w.x[i] = make_double2(x.x * act, x.y * act);
+  if (bits) {
+    uint8_t* dst = bits + i * bits_stride;
+    for (int k = 0; k < bits_stride; ++k) dst[k] = (!dmrs && k < m) ? (uint8_t)((r.x >> k) & 1u) : (uint8_t)0;
+  }
+}
+
+// block = FB subcarriers x (A * T) threads; grid = (ceil(F / FB), B)
+__global__ __launch_bounds__(256) void k_gen_rx(nrx_gen_desc d, GenWs w, int FB, float* __restrict__ y,
+                                                float* __restrict__ h, float* __restrict__ y_re,
+                                                float* __restrict__ y_im) {
+  __shared__ double2 e[4][kMaxUsers * 8];   // phasor of (u, l) at the block's subcarriers
+  const int U = d.num_tx, A = d.num_rx_ant, L = d.num_taps, F = d.num_subcarriers, T = d.num_symbols;
+  const int b = blockIdx.y;
+  const int fl = threadIdx.x / (A * T);
+  const int f = blockIdx.x * FB + fl;
+  for (int j = threadIdx.x; j < FB * U * L; j += blockDim.x) {
+    const int ff = blockIdx.x * FB + j / (U * L);
+    const int ul = j % (U * L);
+    if (ff < F) {
+      const double fa = 2.0 * kPi * (((double)ff * d.subcarrier_spacing) * w.tau[(size_t)b * U * L + ul]);
+      e[j / (U * L)][ul] = make_double2(cos(fa), -sin(fa));
+    }
+  }
+  __syncthreads();
+  if (fl >= FB || f >= F) return;
+  const int at = threadIdx.x % (A * T);
+  const int a = at / T, t = at % T;
+  double yr = 0.0, yi = 0.0;
+  for (int u = 0; u < U; ++u) {
+    const double2* g = w.gt + ((((size_t)b * U + u) * A + a) * L) * T + t;
+    double hr = 0.0, hi = 0.0;
+    for (int l = 0; l < L; ++l) {
+      const double2 gl = g[(size_t)l * T], el = e[fl][u * L + l];
+      hr += gl.x * el.x - gl.y * el.y;
+      hi += gl.x * el.y + gl.y * el.x;
+    }
+    const double2 x = w.x[(((size_t)b * U + u) * F + f) * T + t];
+    yr += hr * x.x - hi * x.y;
+    yi += hr * x.y + hi * x.x;
+    if (h) {
+      float* dst = h + ((((size_t)b * U + u) * F + f) * T + t) * 2 * A;
+      dst[a] = (float)hr;
+      dst[A + a] = (float)hi;
+    }
+  }
+  const U4 r = draw(d, b, ST_NOISE, (uint32_t)((a * F + f) * T + t));
+  const double2 z = box_muller(r.x, r.y);
+  const double sd = sqrt(d.no / 2.0);
+  yr += sd * z.x;
+  yi += sd * z.y;
+  const size_t ft = ((size_t)b * F + f) * T + t;
+  y[ft * 2 * A + a] = (float)yr;
+  y[ft * 2 * A + A + a] = (float)yi;
+  if (y_re) {
+    y_re[ft * A + a] = (float)yr;
+    y_im[ft * A + a] = (float)yi;
+  }
+}
+
+// Nearest own pilot of RE (f, t) in Manhattan distance, first in the pilot order
+// (subcarrier-major, then DMRS symbol): the distance is separable over the Cartesian pilot
+// grid, so it is the smallest own-group subcarrier nearest f and the first listed DMRS
+// symbol nearest t (oracle: synth_ref.nearest_pilot, the general argmin).
+__device__ __forceinline__ void nearest_pilot(const nrx_gen_desc& d, int u, int f, int t, int& fp, int& tp) {
+  const int c = d.cdm_group[u];
+  if ((f & 1) == c) fp = f;
+  else fp = f - 1 >= 0 ? f - 1 : f + 1;
+  int best = 1 << 30;
+  tp = d.dmrs_symbols[0];
+  for (int k = 0; k < d.num_dmrs_symbols; ++k) {
+    const int dt = abs(t - d.dmrs_symbols[k]);
+    if (dt < best) {
+      best = dt;
+      tp = d.dmrs_symbols[k];
+    }
+  }
+}
+
+__device__ __forceinline__ double2 ls(const float* y, const GenWs& w, const nrx_gen_desc& d, int64_t b, int u,
+                                      int fp, int tp, int a) {
+  const int U = d.num_tx, F = d.num_subcarriers, T = d.num_symbols, A = d.num_rx_ant;
+  const double2 x = w.x[(((size_t)b * U + u) * F + fp) * T + tp];
+  if (x.x == 0.0 && x.y == 0.0) return make_double2(0.0, 0.0);
+  const size_t ft = ((size_t)b * F + fp) * T + tp;
+  const double yr = y[ft * 2 * A + a], yi = y[ft * 2 * A + A + a];
+  const double den = x.x * x.x + x.y * x.y;
+  return make_double2((yr * x.x + yi * x.y) / den, (yi * x.x - yr * x.y) / den);
+}
+
+// one thread per (b, u, f, t, a)
+__global__ __launch_bounds__(256) void k_gen_ls(nrx_gen_desc d, GenWs w, const float* __restrict__ y,
+                                                float* __restrict__ h_hat) {
+  const int U = d.num_tx, F = d.num_subcarriers, T = d.num_symbols, A = d.num_rx_ant;
+  const int64_t n = (int64_t)d.batch * U * F * T * A;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int a = (int)(i % A);
+  const int64_t r = i / A;
+  const int t = (int)(r % T);
+  const int f = (int)((r / T) % F);
+  const int u = (int)((r / ((int64_t)T * F)) % U);
+  const int64_t b = r / ((int64_t)T * F * U);
+  int fp, tp;
+  nearest_pilot(d, u, f, t, fp, tp);
+  const double2 v = ls(y, w, d, b, u, fp, tp, a);
+  h_hat[r * 2 * A + a] = (float)v.x;
+  h_hat[r * 2 * A + A + a] = (float)v.y;
+}
+
+// Aerial pilot list [B][Npil][U][A], p = (k * nprb + prb) * 6 + j, subcarrier prb*12 + cdm + 2j
+// (nrx.h nrx_aerial_io); one thread per element.
+__global__ __launch_bounds__(256) void k_gen_ls_aerial(nrx_gen_desc d, GenWs w, const float* __restrict__ y,
+                                                       float* __restrict__ h_re, float* __restrict__ h_im) {
+  const int U = d.num_tx, F = d.num_subcarriers, A = d.num_rx_ant;
+  const int nprb = F / 12, npl = d.num_dmrs_symbols * nprb * 6;
+  const int64_t n = (int64_t)d.batch * npl * U * A;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int a = (int)(i % A);
+  const int u = (int)((i / A) % U);
+  const int p = (int)((i / ((int64_t)A * U)) % npl);
+  const int64_t b = i / ((int64_t)A * U * npl);
+  const int j = p % 6, prb = (p / 6) % nprb, k = p / (6 * nprb);
+  const double2 v = ls(y, w, d, b, u, prb * 12 + d.cdm_group[u] + 2 * j, d.dmrs_symbols[k], a);
+  h_re[i] = (float)v.x;
+  h_im[i] = (float)v.y;
+}
+
+// one workgroup per (b, u): bit errors of the head's hard decisions on the data REs
+__global__ __launch_bounds__(256) void k_count_errors(nrx_count_io c) {
+  __shared__ unsigned long long red[256];
+  const int U = c.num_tx, F = c.num_subcarriers, T = c.num_symbols, BS = c.bits_stride;
+  const int64_t bu = blockIdx.x;
+  const int u = (int)(bu % U);
+  if (c.active[bu] <= 0.0f) return;            // uniform per block
+  const int m = c.mcs ? c.mcs[bu] : 0;
+  const int nb = c.mcs_bits[m];
+  const int head = c.num_heads > 1 ? m : 0;
+  const float* l = c.llr + ((size_t)head * c.batch * U + bu) * (size_t)F * T * BS;
+  const uint8_t* s = c.bits + (size_t)bu * F * T * BS;
+  unsigned long long err = 0;
+  for (int i = threadIdx.x; i < F * T; i += 256) {
+    const int t = i % T;
+    if ((c.dmrs_symbol_mask >> t) & 1) continue;
+    for (int k = 0; k < nb; ++k) err += (uint8_t)(l[(size_t)i * BS + k] > 0.0f) != s[(size_t)i * BS + k];
+  }
+  red[threadIdx.x] = err;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const unsigned long long e = red[0];
+    unsigned long long* o = reinterpret_cast<unsigned long long*>(c.counts) + 4 * u;
+    atomicAdd(o + 0, e);
+    atomicAdd(o + 2, e ? 1ull : 0ull);
+    atomicAdd(o + 3, 1ull);
+  }
+  if (threadIdx.x == 1) {   // bits compared = data REs x bits of this (slot, user)
+    unsigned long long n = 0;
+    for (int t = 0; t < T; ++t)
+      if (!((c.dmrs_symbol_mask >> t) & 1)) n += (unsigned long long)F * nb;
+    atomicAdd(reinterpret_cast<unsigned long long*>(c.counts) + 4 * u + 1, n);
+  }
+}
+
+size_t al(size_t x) { return (x + 255) / 256 * 256; }
+
+}  // namespace
+
+size_t gen_workspace_bytes(const nrx_gen_desc& d, GenWs* w, char* base) {
+  const size_t B = d.batch, U = d.num_tx, F = d.num_subcarriers, T = d.num_symbols, A = d.num_rx_ant,
+               L = d.num_taps;
+  size_t o = 0;
+  auto take = [&](size_t n) {
+    char* p = base ? base + o : nullptr;
+    o += al(n);
+    return p;
+  };
+  GenWs v;
+  v.x = (double2*)take(B * U * F * T * sizeof(double2));
+  v.gt = (double2*)take(B * U * A * L * T * sizeof(double2));
+  v.tau = (double*)take(B * U * L * sizeof(double));
+  v.spdp = (double*)take(B * U * L * sizeof(double));
+  v.mcs = (uint8_t*)take(B * U);
+  v.active = (float*)take(B * U * sizeof(float));
+  if (w) *w = v;
+  return o;
+}
+
+hipError_t launch_generate(const nrx_gen_desc& d, const nrx_gen_out& o, void* ws, hipStream_t st) {
+  GenWs w;
+  gen_workspace_bytes(d, &w, (char*)ws);
+  const int64_t B = d.batch, U = d.num_tx, F = d.num_subcarriers, T = d.num_symbols, A = d.num_rx_ant,
+                L = d.num_taps;
+  auto blocks = [](int64_t n) { return (unsigned)((n + 255) / 256); };
+  k_gen_params<<<(unsigned)B, 64, 0, st>>>(d, w, o.active, o.mcs_mask, o.mcs);
+  k_gen_taps<<<blocks(B * U * A * L), 256, 0, st>>>(d, w);
+  k_gen_tx<<<blocks(B * U * F * T), 256, 0, st>>>(d, w, o.bits, o.bits_stride);
+  const int at = (int)(A * T);
+  int FB = 256 / at;
+  if (FB > 4) FB = 4;
+  k_gen_rx<<<dim3((unsigned)((F + FB - 1) / FB), (unsigned)B), FB * at, 0, st>>>(d, w, FB, o.y, o.h, o.y_real,
+                                                                                o.y_imag);
+  if (o.h_hat) k_gen_ls<<<blocks(B * U * F * T * A), 256, 0, st>>>(d, w, o.y, o.h_hat);
+  if (o.h_ls_real)
+    k_gen_ls_aerial<<<blocks(B * d.num_dmrs_symbols * (F / 12) * 6 * U * A), 256, 0, st>>>(d, w, o.y, o.h_ls_real,
+                                                                                          o.h_ls_imag);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_errors(const nrx_count_io& c, hipStream_t st) {
+  k_count_errors<<<(unsigned)((int64_t)c.batch * c.num_tx), 256, 0, st>>>(c);
+  return hipGetLastError();
+}
+
+}  // namespace nrx
