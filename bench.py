@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-latency", action="store_true")
+    p.add_argument("--no-e2e", action="store_true", help="skip the generate+receive+count measurement")
     p.add_argument("--graph", action="store_true",
                    help="time replays of a captured hipGraph instead of direct nrx_forward calls")
     p.add_argument("--profile-only", action="store_true",
@@ -180,6 +181,11 @@ def main():
         latency = measure_latency(torch, eng, spec, cfg, args, groups, dev, num_it)
         latency["132prb_aerial_contract"] = measure_latency_aerial(torch, eng, spec, cfg, args, groups, dev, num_it)
 
+    # ---- end-to-end Monte-Carlo step on the GPU: generate + receive + count (not `value`)
+    e2e = None
+    if not args.no_e2e:
+        e2e = measure_e2e(torch, eng, spec, cfg, args, dev, num_it, rank, world)
+
     # ---- CPU baseline: the numpy oracle (fp32) on a bounded sample of the same workload
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
@@ -206,12 +212,54 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "p50_latency_ms": latency,
+            "e2e_generate_receive_count": e2e,
             "whole_forward_tflops": round(whole_tflops, 2),
             "kernels": kern,
         }
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def measure_e2e(torch, eng, spec, cfg, args, dev, num_it, rank, world):
+    """One evaluation-loop step per batch, all on the GPU (neural_rx_amd.evaluate.sim_ber):
+    the slot generator (nrx_generate_slots: bits, QAM, TDL channel, AWGN, LS+NN h_hat),
+    the CGNN forward and the uncoded error counters (nrx_count_errors).  Same batch/shape as
+    the headline; each rank generates its own slots (global slot index), no collective in
+    the timed loop.  Reported beside the headline, never as `value`."""
+    from neural_rx_amd.generator import GenParams, SlotGenerator, count_errors, ebno_to_no
+    from neural_rx_amd.receiver import compute_pe
+    B, U = args.batch, args.users
+    p = GenParams.from_config(cfg, num_tx=U, num_prbs=args.prbs)
+    gen = SlotGenerator(p, device=int(dev.split(":")[1]))
+    no = ebno_to_no(4.0)
+    pe = torch.from_numpy(compute_pe(U, p.num_subcarriers, p.dmrs_symbols, p.cdm_group)).to(dev)
+    out = eng.alloc_outputs(B, U, p.num_subcarriers, want_h=False)
+    counts = torch.zeros((U, 4), dtype=torch.int64, device=dev)
+
+    def one(i):
+        sb = gen(B, no, slot_offset=(i * world + rank) * B)
+        llr, _ = eng.forward(sb.y, pe, sb.h_hat, sb.active, None, num_it, args.precision, out=out, want_h=False)
+        count_errors(llr, sb.bits, sb.active, sb.mcs, p.mcs_bits, p.dmrs_symbols, counts=counts)
+
+    for i in range(args.warmup):
+        one(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        one(args.warmup + i)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    for i in range(args.steps):
+        gen(B, no, slot_offset=i * B)
+    torch.cuda.synchronize()
+    gen_el = time.perf_counter() - t1
+    c = counts.sum(0).cpu().numpy()
+    return {"slots_per_s_per_gpu": round(B * args.steps / el, 1), "ms_per_step": round(1e3 * el / args.steps, 4),
+            "generator_ms_per_batch": round(1e3 * gen_el / args.steps, 4), "ebno_db": 4.0,
+            "uncoded_ber": float(c[0] / c[1]) if c[1] else None,
+            "note": "GPU slot generator + CGNN forward + error counters per step (evaluate.sim_ber)"}
 
 
 def measure_latency(torch, eng, spec, cfg, args, groups, dev, num_it):

@@ -7,14 +7,14 @@
 //
 //   k_gen_params   per slot: active ports (Fisher-Yates, e2e_model.py:187-193), MCS per
 //                  user, TDL delays (sorted, first = 0) and the exponential PDP
-//   k_gen_taps     per (slot, user, antenna, tap): sum-of-sinusoids tap gain g(t), T values
+//   k_gen_taps     per (slot, user, antenna, tap, symbol): sum-of-sinusoids tap gain g(t)
 //   k_gen_tx       per (slot, user, RE): Philox bits, Gray QAM / DMRS QPSK x sqrt(2), x *= active
 //   k_gen_rx       per (slot, subcarrier): the user/tap phasors of that subcarrier in LDS,
 //                  then y[a][t] = sum_u H_u x_u + AWGN (and the true channel, optional)
 //   k_gen_ls       per (slot, user, RE, antenna): LS at the nearest own pilot (closed form
 //                  of the Manhattan argmin), and the Aerial pilot list (optional)
-//   k_count_errors per (slot, user): hard decisions of the LLR head vs the sent bits on the
-//                  data REs, block reduction, 4 int64 atomics
+//   k_count_errors per (slot group, user): hard decisions of the LLR head vs the sent bits on
+//                  the data REs, block reductions, 4 int64 atomics per workgroup
 //
 // Random draws: Philox4x32-10 with key = seed and counter = (element, slot lo, slot hi,
 // stream), slot = slot_offset + b -- a pure function of the global slot index, so any split
@@ -127,59 +127,77 @@ __global__ __launch_bounds__(64) void k_gen_params(nrx_gen_desc d, GenWs w, floa
     if (mcs_out) mcs_out[b * U + u] = (uint8_t)m;
     if (mcs_mask)
       for (int k = 0; k < M; ++k) mcs_mask[((size_t)b * U + u) * M + k] = k == m ? 1.0f : 0.0f;
-    double tau[8];
-    for (int l = 0; l < L; ++l) tau[l] = uni(draw(d, b, ST_DELAY, u * L + l).x) * d.max_delay_s;
-    for (int l = 1; l < L; ++l) {   // insertion sort (ascending)
-      const double v = tau[l];
-      int k = l - 1;
-      while (k >= 0 && tau[k] > v) {
-        tau[k + 1] = tau[k];
-        --k;
-      }
-      tau[k + 1] = v;
+  }
+  // delays: one thread per (u, l) (U * L <= 128 = 2 passes of 64); ascending order by rank
+  // (ties by index, as a stable sort), the smallest set to 0; PDP normalised per user
+  __shared__ double tau[kMaxUsers * 8];
+  __shared__ double pw[kMaxUsers * 8];
+  for (int j = i; j < U * L; j += 64) tau[j] = uni(draw(d, b, ST_DELAY, j).x) * d.max_delay_s;
+  __syncthreads();
+  double tr[2], pr[2];
+  int rk[2];
+  for (int q = 0; q < 2; ++q) {
+    const int j = i + 64 * q;
+    if (j >= U * L) break;
+    const int u = j / L, l = j % L;
+    int r = 0;
+    for (int k = 0; k < L; ++k) {
+      const double o = tau[u * L + k];
+      r += (o < tau[j]) || (o == tau[j] && k < l);
     }
-    tau[0] = 0.0;
-    double p[8], ps = 0.0;
-    for (int l = 0; l < L; ++l) {
-      p[l] = exp(-tau[l] / (d.max_delay_s / kPDP + 1e-12));
-      ps += p[l];
-    }
-    for (int l = 0; l < L; ++l) {
-      w.tau[(b * U + u) * L + l] = tau[l];
-      w.spdp[(b * U + u) * L + l] = sqrt(p[l] / ps);
-    }
+    rk[q] = r;
+    tr[q] = r == 0 ? 0.0 : tau[j];
+    pr[q] = exp(-tr[q] / (d.max_delay_s / kPDP + 1e-12));
+  }
+  __syncthreads();
+  for (int q = 0; q < 2; ++q) {
+    const int j = i + 64 * q;
+    if (j >= U * L) break;
+    const int u = j / L;
+    tau[u * L + rk[q]] = tr[q];
+    pw[u * L + rk[q]] = pr[q];
+  }
+  __syncthreads();
+  for (int q = 0; q < 2; ++q) {
+    const int j = i + 64 * q;
+    if (j >= U * L) break;
+    const int u = j / L;
+    double ps = 0.0;
+    for (int k = 0; k < L; ++k) ps += pw[u * L + k];
+    w.tau[(size_t)b * U * L + j] = tau[j];
+    w.spdp[(size_t)b * U * L + j] = sqrt(pw[j] / ps);
   }
 }
 
-// one thread per (b, u, a, l): g(t) = sqrt(pdp_l) sum_s g0_s exp(j 2 pi fd_s t Tsym)
+// one thread per (b, u, a, l, t): g(t) = sqrt(pdp_l) sum_s g0_s exp(j 2 pi fd_s t Tsym)
+// (the sinusoid draws are recomputed per t: 14x more threads instead of a serial t loop of
+// f64 sin/cos per thread, which left this launch latency-bound)
 __global__ __launch_bounds__(256) void k_gen_taps(nrx_gen_desc d, GenWs w) {
   const int U = d.num_tx, A = d.num_rx_ant, L = d.num_taps, NS = d.num_sinusoids, T = d.num_symbols;
-  const int64_t n = (int64_t)d.batch * U * A * L;
+  const int64_t n = (int64_t)d.batch * U * A * L * T;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const int l = (int)(i % L);
-  const int a = (int)((i / L) % A);
-  const int u = (int)((i / ((int64_t)L * A)) % U);
-  const int64_t b = i / ((int64_t)L * A * U);
+  const int t = (int)(i % T);
+  const int64_t bual = i / T;
+  const int l = (int)(bual % L);
+  const int a = (int)((bual / L) % A);
+  const int u = (int)((bual / ((int64_t)L * A)) % U);
+  const int64_t b = bual / ((int64_t)L * A * U);
   const double tsym = kCP / d.subcarrier_spacing;
-  double2 acc[kT];
-  for (int t = 0; t < T; ++t) acc[t] = make_double2(0.0, 0.0);
+  const double sc = 1.0 / sqrt(2.0 * NS);
+  double ar = 0.0, ai = 0.0;
   for (int s = 0; s < NS; ++s) {
     const U4 r = draw(d, b, ST_TAP, (uint32_t)((((u * A + a) * L + l) * NS) + s));
     const double2 z = box_muller(r.x, r.y);
-    const double sc = 1.0 / sqrt(2.0 * NS);
     const double g0r = z.x * sc, g0i = z.y * sc;
     const double fd = d.max_doppler_hz * cos(2.0 * kPi * uni(r.z));
-    for (int t = 0; t < T; ++t) {
-      const double ph = 2.0 * kPi * (fd * (t * tsym));
-      const double c = cos(ph), sn = sin(ph);
-      acc[t].x += g0r * c - g0i * sn;
-      acc[t].y += g0r * sn + g0i * c;
-    }
+    const double ph = 2.0 * kPi * (fd * (t * tsym));
+    const double c = cos(ph), sn = sin(ph);
+    ar += g0r * c - g0i * sn;
+    ai += g0r * sn + g0i * c;
   }
   const double sp = w.spdp[(b * U + u) * L + l];
-  double2* dst = w.gt + i * T;
-  for (int t = 0; t < T; ++t) dst[t] = make_double2(acc[t].x * sp, acc[t].y * sp);
+  w.gt[i] = make_double2(ar * sp, ai * sp);
 }
 
 // one thread per (b, u, f, t)
@@ -333,42 +351,52 @@ __global__ __launch_bounds__(256) void k_gen_ls_aerial(nrx_gen_desc d, GenWs w, 
   h_im[i] = (float)v.y;
 }
 
-// one workgroup per (b, u): bit errors of the head's hard decisions on the data REs
-__global__ __launch_bounds__(256) void k_count_errors(nrx_count_io c) {
-  __shared__ unsigned long long red[256];
+__device__ __forceinline__ unsigned wave_sum(unsigned v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// grid (G, U): workgroup (g, u) walks the slots b = g, g + G, ... of user u; per (b, u) a
+// block reduction gives the bit errors (and whether the grid has any), accumulated in
+// registers; 3 int64 atomics per workgroup at the end (G <= 32 keeps same-address atomics
+// few: the per-(b, u) atomics of a one-block-per-grid layout serialised at L2)
+__global__ __launch_bounds__(256) void k_count_errors(nrx_count_io c, int G) {
+  __shared__ unsigned red[4];
   const int U = c.num_tx, F = c.num_subcarriers, T = c.num_symbols, BS = c.bits_stride;
-  const int64_t bu = blockIdx.x;
-  const int u = (int)(bu % U);
-  if (c.active[bu] <= 0.0f) return;            // uniform per block
-  const int m = c.mcs ? c.mcs[bu] : 0;
-  const int nb = c.mcs_bits[m];
-  const int head = c.num_heads > 1 ? m : 0;
-  const float* l = c.llr + ((size_t)head * c.batch * U + bu) * (size_t)F * T * BS;
-  const uint8_t* s = c.bits + (size_t)bu * F * T * BS;
-  unsigned long long err = 0;
-  for (int i = threadIdx.x; i < F * T; i += 256) {
-    const int t = i % T;
-    if ((c.dmrs_symbol_mask >> t) & 1) continue;
-    for (int k = 0; k < nb; ++k) err += (uint8_t)(l[(size_t)i * BS + k] > 0.0f) != s[(size_t)i * BS + k];
-  }
-  red[threadIdx.x] = err;
-  __syncthreads();
-  for (int st = 128; st > 0; st >>= 1) {
-    if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+  const int u = blockIdx.y;
+  unsigned long long err_tot = 0, bits_tot = 0, blk_err = 0, blks = 0;
+  int ndata = 0;
+  for (int t = 0; t < T; ++t) ndata += !((c.dmrs_symbol_mask >> t) & 1);
+  for (int b = blockIdx.x; b < c.batch; b += G) {
+    const int64_t bu = (int64_t)b * U + u;
+    if (c.active[bu] <= 0.0f) continue;        // uniform per block
+    const int m = c.mcs ? c.mcs[bu] : 0;
+    const int nb = c.mcs_bits[m];
+    const int head = c.num_heads > 1 ? m : 0;
+    const float* l = c.llr + ((size_t)head * c.batch * U + bu) * (size_t)F * T * BS;
+    const uint8_t* sb = c.bits + (size_t)bu * F * T * BS;
+    unsigned err = 0;
+    for (int i = threadIdx.x; i < F * T; i += 256) {
+      if ((c.dmrs_symbol_mask >> (i % T)) & 1) continue;
+      for (int k = 0; k < nb; ++k) err += (uint8_t)(l[(size_t)i * BS + k] > 0.0f) != sb[(size_t)i * BS + k];
+    }
+    err = wave_sum(err);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = err;
     __syncthreads();
+    const unsigned e = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    err_tot += e;
+    bits_tot += (unsigned long long)ndata * F * nb;
+    blk_err += e ? 1 : 0;
+    blks += 1;
   }
-  if (threadIdx.x == 0) {
-    const unsigned long long e = red[0];
+  if (threadIdx.x == 0 && blks) {
     unsigned long long* o = reinterpret_cast<unsigned long long*>(c.counts) + 4 * u;
-    atomicAdd(o + 0, e);
-    atomicAdd(o + 2, e ? 1ull : 0ull);
-    atomicAdd(o + 3, 1ull);
-  }
-  if (threadIdx.x == 1) {   // bits compared = data REs x bits of this (slot, user)
-    unsigned long long n = 0;
-    for (int t = 0; t < T; ++t)
-      if (!((c.dmrs_symbol_mask >> t) & 1)) n += (unsigned long long)F * nb;
-    atomicAdd(reinterpret_cast<unsigned long long*>(c.counts) + 4 * u + 1, n);
+    atomicAdd(o + 0, err_tot);
+    atomicAdd(o + 1, bits_tot);
+    atomicAdd(o + 2, blk_err);
+    atomicAdd(o + 3, blks);
   }
 }
 
@@ -403,7 +431,7 @@ hipError_t launch_generate(const nrx_gen_desc& d, const nrx_gen_out& o, void* ws
                 L = d.num_taps;
   auto blocks = [](int64_t n) { return (unsigned)((n + 255) / 256); };
   k_gen_params<<<(unsigned)B, 64, 0, st>>>(d, w, o.active, o.mcs_mask, o.mcs);
-  k_gen_taps<<<blocks(B * U * A * L), 256, 0, st>>>(d, w);
+  k_gen_taps<<<blocks(B * U * A * L * T), 256, 0, st>>>(d, w);
   k_gen_tx<<<blocks(B * U * F * T), 256, 0, st>>>(d, w, o.bits, o.bits_stride);
   const int at = (int)(A * T);
   int FB = 256 / at;
@@ -418,7 +446,8 @@ hipError_t launch_generate(const nrx_gen_desc& d, const nrx_gen_out& o, void* ws
 }
 
 hipError_t launch_count_errors(const nrx_count_io& c, hipStream_t st) {
-  k_count_errors<<<(unsigned)((int64_t)c.batch * c.num_tx), 256, 0, st>>>(c);
+  const int G = c.batch < 32 ? c.batch : 32;
+  k_count_errors<<<dim3(G, c.num_tx), 256, 0, st>>>(c, G);
   return hipGetLastError();
 }
 
