@@ -614,6 +614,7 @@ struct BlockParams {
   int strips;                                            // strips per (slot, user)
   int order_rev;                                         // XCD-local work order reversed
   int inline_combine;                                    // U <= kInlineUsers: z-load forms a
+  int norm_pre;                                          // a.norm[b] holds the slot norm (k_norm ran)
 };
 
 template <class P>
@@ -1138,6 +1139,31 @@ __device__ __forceinline__ double slot_norm(const float* y, int nq, double* red)
   return ms > 0.0 ? 1.0 / sqrt(ms) : 0.0;
 }
 
+// Per-slot normalisation pass for large grids (one workgroup per slot, fixed striding and
+// reduction order: deterministic).  norm[b] = 1/sqrt(mean(y^2)), 0 for an all-zero slot.
+__global__ __launch_bounds__(1024) void k_norm(const float* __restrict__ y, int nq, double* __restrict__ norm) {
+  __shared__ double red[16];
+  const floatx4* yq = reinterpret_cast<const floatx4*>(y) + (size_t)blockIdx.x * nq;
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nq; i += 1024) {
+    const floatx4 v = yq[i];
+    acc += (double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2] + (double)v[3] * v[3];
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot = 0.0;
+    for (int w = 0; w < 16; ++w) tot += red[w];
+    const double ms = tot / (double)(4 * nq);
+    norm[blockIdx.x] = ms > 0.0 ? 1.0 / sqrt(ms) : 0.0;
+  }
+}
+
+// slot grids above this many float4s get the separate k_norm pass (nrx_rt: 1 344)
+constexpr int kNormFusedMaxQ = 8192;
+
 template <class P, int A2P, int CHP, int TAILM>
 __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem, int b, int u,
                                           int strip, typename P::Real wm, bool first) {
@@ -1187,7 +1213,9 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
       hv[2 * k + 1] = w.y;
     }
     if (ok) pv = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + f) * kT + tt) * 2);
-    const Real ns = (Real)slot_norm(a.y + (size_t)b * F * kT * A2, F * kT * A2 / 4, red);
+    // large grids: the per-slot k_norm pass already reduced y (every workgroup of the slot
+    // re-reading the whole grid costs O(strips x grid) there); small grids: fused here
+    const Real ns = prm.norm_pre ? (Real)a.norm[b] : (Real)slot_norm(a.y + (size_t)b * F * kT * A2, F * kT * A2 / 4, red);
     if (lf < R0) {
 #pragma unroll
       for (int q = 0; q < NQZ; ++q) {
@@ -1494,6 +1522,13 @@ struct Launch {
     bp.a = args;
     bp.inline_combine = args.U <= kInlineUsers;
     bp.strips = strips;
+    const int nq = args.F * kT * 2 * args.A / 4;
+    bp.norm_pre = nq > kNormFusedMaxQ;
+    if (bp.norm_pre) {
+      B_(K_NORM);
+      k_norm<<<args.B, 1024, 0, st>>>(args.y, nq, args.norm);
+      E_(K_NORM);
+    }
     int launch_no = 0;
     // U > kInlineUsers: the leave-one-out combine runs as its own launch on the sp rows
     auto combine = [&](typename P::S* sp) {

@@ -89,6 +89,15 @@ def test_all_zero_slot():
     check_both(case)
 
 
+def test_large_grid_separate_norm_pass():
+    # 25 PRB x 4 antennas: the slot grid exceeds the fused-normalisation limit, so the
+    # per-slot k_norm pass runs before StateInit (one slot all-zero: divide-no-nan)
+    case = make_case("nrx_rt", batch=2, users=1, prbs=25, snr_db=12)
+    case.y[0] = 0
+    case.h_hat[0] = 0
+    check_both(case)
+
+
 def test_var_io_mixed_mcs():
     check_both(make_case("nrx_rt_var_mcs", batch=4, users=2, prbs=4,
                          mcs_choice=[[0, 1], [1, 0], [1, 1], [0, 0]]))

@@ -1,0 +1,98 @@
+"""Per-GPU forward throughput at every BASELINE.json configuration (one MI355X).
+
+    python tools/bench_configs.py [--steps K] [--out FILE]
+
+bench.py measures the headline (configs[1]); this reports the other configurations' per-GPU
+shard as a table for DESIGN.md: slots/s, ms per batch, whole-forward algorithmic TFLOP/s
+and its fraction of the f16 MFMA peak.  Inputs come from the GPU slot generator
+(nrx_generate_slots), so even the 273-PRB / 8-user shard needs no host-side data.
+Config 3 (16 rx antennas) has no trained weights: seeded weights of that topology.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# (tag, config, users, PRBs, rx antennas, slots per GPU, var_mcs, seeded weights)
+CONFIGS = [
+    ("cfg1 nrx_rt 1UE 4PRB B=1", "nrx_rt", 1, 4, 4, 1, False, False),
+    ("cfg2 nrx_rt 2UE 4PRB B=128", "nrx_rt", 2, 4, 4, 128, False, False),
+    ("cfg3 nrx_large 4UE 132PRB 16ant B=64", "nrx_large", 4, 132, 16, 64, False, True),
+    ("cfg4 nrx_rt_var_mcs 2UE 4PRB B=1024/8", "nrx_rt_var_mcs", 2, 4, 4, 128, True, False),
+    ("cfg4' nrx_large_var_mcs_64qam_masking 2UE 4PRB B=1024/8", "nrx_large_var_mcs_64qam_masking", 2, 4, 4, 128,
+     True, False),
+    ("cfg5 nrx_large_64qam 8UE 273PRB B=256/8", "nrx_large_64qam", 8, 273, 4, 32, False, False),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--only", default=None, help="substring of the config tag")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import torch
+    from neural_rx_amd import metrics
+    from neural_rx_amd import weights as W
+    from neural_rx_amd.config import get_config, spec_from_config
+    from neural_rx_amd.generator import GenParams, SlotGenerator, ebno_to_no
+    from neural_rx_amd.receiver import CGNNEngine, compute_pe
+    dev = "cuda:0"
+    rows = []
+    for tag, name, U, prbs, ant, B, var, seeded in CONFIGS:
+        if a.only and a.only not in tag:
+            continue
+        cfg = get_config(name)
+        spec = spec_from_config(cfg, ant)
+        wl = W.seeded(spec, seed=3) if seeded else W.load(cfg.label)
+        eng = CGNNEngine(spec, wl)
+        p = GenParams.from_config(cfg, num_tx=U, num_prbs=prbs, num_rx_ant=ant, var_mcs=var, seed=5)
+        gen = SlotGenerator(p)
+        sb = gen(B, ebno_to_no(6.0))
+        pe = torch.from_numpy(compute_pe(U, p.num_subcarriers, p.dmrs_symbols, p.cdm_group)).to(dev)
+        num_it = cfg.num_nrx_iter_eval
+        mm = sb.mcs_mask if spec.num_mcs > 1 else None
+        out = eng.alloc_outputs(B, U, p.num_subcarriers)
+        step = lambda: eng.forward(sb.y, pe, sb.h_hat, sb.active, mm, num_it, "f16", out=out)  # noqa: E731
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / a.steps
+        eng.profile(True)
+        for _ in range(a.steps):
+            step()
+        prof = eng.profile_read()
+        eng.profile(False)
+        re_users = B * U * p.num_subcarriers * 14
+        fl = metrics.forward_flops_per_re_user(spec, num_it) * re_users
+        kfl = metrics.launch_flops_per_re_user(spec, num_it)
+        kern = {k: {"launches": n, "avg_us": round(ms / n * 1e3, 2),
+                    "tflops": round(kfl[k] * re_users / (ms / n * 1e-3) / 1e12, 1) if kfl[k] else None}
+                for k, (n, ms) in prof.items() if n}
+        row = {"config": tag, "slots_per_gpu": B, "num_it": num_it, "ms_per_batch": round(el * 1e3, 4),
+               "slots_per_s_per_gpu": round(B / el, 1), "gflop_per_batch": round(fl / 1e9, 2),
+               "whole_forward_tflops": round(fl / el / 1e12, 1),
+               "frac_f16_mfma_peak": round(fl / el / 1e12 / metrics.PEAK_TFLOPS["f16"], 4), "kernels": kern}
+        print(json.dumps(row), flush=True)
+        rows.append(row)
+        eng.close()
+        del sb, out, gen
+        torch.cuda.empty_cache()
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
