@@ -41,7 +41,9 @@
 
 #ifndef NRX_ABLATE
 #define NRX_ABLATE 0   // diagnostic builds only: 1 skip conv math, 2 skip z loads, 4 skip weight
-                       // staging, 8 skip tails, 16 skip conv3 global epilogue
+                       // staging, 8 skip tails, 16 skip conv3 global epilogue, 32 skip the
+                       // state stores, 64 skip the act*sp stores (MLP still computed), 128
+                       // skip the aggregation MLP (stores kept)
 #endif
 
 namespace nrx {
@@ -904,7 +906,7 @@ struct EpiConv3 {
       for (int r = 0; r < R; ++r) {
         S* dst = a.s_out + off[r];
         if constexpr (sizeof(S) == 2) {
-          store_row16(dst, sv[r], ok[r], g);
+          store_row16(dst, sv[r], ok[r] && !((NRX_ABLATE & 32) && a.B > 0), g);
         } else {
           if (!ok[r]) continue;
 #pragma unroll
@@ -926,7 +928,14 @@ struct EpiConv3 {
       Real hdn[R][kAGG / 16][4], sp[R][NTS][4];
       const Real act = (Real)a.active[(size_t)b * U + u];
       CFrag<P, kAGG / 16> hb[R];
-      if constexpr (P::WLDS) {
+      if constexpr ((NRX_ABLATE & 128) != 0 && P::WLDS) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+          for (int n = 0; n < NTS; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) sp[r][n][j] = sv[r][n][j];
+      } else if constexpr (P::WLDS) {
         DLds<P, kDSP> w1{WB + 16 * 1024, reinterpret_cast<const float*>(WB + kWTailBias)};
         DLds<P, kAGG> w2{WB + 24 * 1024, reinterpret_cast<const float*>(WB + kWTailBias + kAGG * 4)};
         dense_rows<P, NTS, kAGG, R>(sb, w1, lane, g, hdn, true);
@@ -948,7 +957,7 @@ struct EpiConv3 {
           for (int n = 0; n < NTS; ++n)
 #pragma unroll
             for (int j = 0; j < 4; ++j) spa[n][j] = sp[r][n][j] * act;
-          store_row16(dst, spa, ok[r], g);
+          store_row16(dst, spa, ok[r] && !((NRX_ABLATE & 64) && a.B > 0), g);
         } else {
           if (!ok[r]) continue;
 #pragma unroll
@@ -1259,15 +1268,18 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
   // U <= kInlineUsers (AggregateUserStates' leave-one-out mean, neural_rx.py:191-204);
   // otherwise k_combine already wrote a_u in place.
   // The in-grid rows [lo, hi) of a (b, u) plane are one contiguous range of the compact
-  // [F][14][56] layout, so chunk c of it is simply base + 16 c: all global loads are
-  // issued first (32-bit offsets from a wave-uniform base), then the LDS stores.
+  // [F][14][56] layout (K = 14 * QS chunks per row).  Fixed thread -> (row phase, symbol,
+  // chunk) mapping: thread tid handles chunk k = tid % K of image rows r = tid / K + RG * i,
+  // so per iteration only the row advances (one add on the global and on the LDS offset; no
+  // divisions) and rows outside the grid store zeros in the same pass.  All global loads are
+  // issued first (32-bit offsets from wave-uniform bases), then the LDS stores.
   using Real = typename P::Real;
-  constexpr int NV_MAX = R0 * kT * QS;
-  constexpr int PV = (NV_MAX + 511) / 512;
+  constexpr int K = kT * QS;               // chunks per row of one plane
+  constexpr int RG = 512 / K;              // image rows per iteration (P16: 5, P64: 2)
+  constexpr int PV = (R0 + RG - 1) / RG;   // iterations (P16: 6, P64: 7)
   const int lo = f_start < 0 ? 0 : f_start;
   const int hi = f_start + R0 < F ? f_start + R0 : F;
   const int slot_lo = lo - f_start, nrow = hi - lo;
-  const unsigned NV = (unsigned)(nrow * kT * QS);
   const bool inl = prm.inline_combine != 0;
   // planes read for a: inline -> the U-1 other users' act*sp rows; else the combined a_u
   const int no = inl ? U - 1 : 1;
@@ -1280,12 +1292,15 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
     const int uu = inl ? (k < u ? k : k + 1) : u;
     ab[k] = reinterpret_cast<const intx4*>(a.a + srow(b, uu < U ? uu : 0, lo, 0, U, F));
   }
+  const int kk = threadIdx.x % K, r0 = threadIdx.x / K;
+  const bool lane_on = r0 < RG;
+  const int tk = kk / QS, qk = kk % QS;
   intx4 vs[PV], va[PV][kInlineUsers - 1];
 #pragma unroll
   for (int i = 0; i < PV; ++i) {
-    unsigned c = threadIdx.x + 512u * i;
-    if (NRX_ABLATE & 2) c = 0;
-    c = c < NV ? c : 0;          // tail lanes re-read chunk 0 and store nothing
+    const int rr = r0 + RG * i - slot_lo;           // plane row of image row r0 + RG i
+    const bool ld = lane_on && rr >= 0 && rr < nrow && !(NRX_ABLATE & 2);
+    const unsigned c = ld ? (unsigned)(rr * K + kk) : 0u;   // clamped: chunk 0, not stored
     vs[i] = sb[c];
 #pragma unroll
     for (int k = 0; k < kInlineUsers - 1; ++k) va[i][k] = k < no ? ab[k][c] : intx4{0, 0, 0, 0};
@@ -1300,37 +1315,24 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
   const float2 pe_v = *reinterpret_cast<const float2*>(
       a.pe + (((size_t)u * F + (pe_ok ? pe_f : 0)) * kT + (pe_ok ? pe_t : 0)) * 2);
   stamp(24);
-  // fixed zero chunks while the loads fly: t = 14, 15 (all chunks) and, for t < 14, the
-  // pad chunks (2QS, NQ) (the pe chunk 2QS is overwritten below)
+  // zero chunks while the loads fly: the pad symbols t = 14, 15 of every slot are one
+  // contiguous 2 * NQ-chunk block at the end of the slot's symbol rows (whatever the swizzle)
   {
-    constexpr int NX = NQ - 2 * QS;                  // pe + pad chunks per symbol
-    constexpr int PER_SLOT = 2 * NQ + kT * NX;
-    for (int idx = threadIdx.x; idx < R0 * PER_SLOT; idx += 512) {
-      const int slot = idx / PER_SLOT, k = idx % PER_SLOT;
-      int tt, q;
-      if (k < 2 * NQ) {
-        tt = kT + k / NQ;
-        q = k % NQ;
-      } else {
-        tt = (k - 2 * NQ) / NX;
-        q = 2 * QS + (k - 2 * NQ) % NX;
-      }
-      if (q != 2 * QS || tt >= kT) *reinterpret_cast<intx4*>(X + xoff<P, NQ>(slot, tt, q)) = intx4{0, 0, 0, 0};
-    }
-    // a / s chunks of the slots outside the grid (edge strips only)
-    const int nout = R0 - nrow;
-    for (int idx = threadIdx.x; idx < nout * kT * 2 * QS; idx += 512) {
-      const int j = idx / (kT * 2 * QS), k = idx % (kT * 2 * QS);
-      const int slot = j < slot_lo ? j : nrow + j;
-      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(slot, k / (2 * QS), k % (2 * QS))) = intx4{0, 0, 0, 0};
-    }
+    constexpr int ZS = 2 * NQ;                       // chunks per slot (power of 2)
+    static_assert((ZS & (ZS - 1)) == 0, "pad block size");
+    for (int idx = threadIdx.x; idx < R0 * ZS; idx += 512)
+      *reinterpret_cast<intx4*>(X + (idx / ZS) * slot_pitch<P>() + (kT * NQ + idx % ZS) * 16) = intx4{0, 0, 0, 0};
   }
   stamp(25);
   if (pe_slot < R0) {
+    // pe chunk 2QS and the pad chunks (2QS, NQ) of symbol row (pe_slot, pe_t)
     S pe2[P::EPC] = {};
     pe2[0] = pe_ok ? (S)pe_v.x : (S)0;
     pe2[1] = pe_ok ? (S)pe_v.y : (S)0;
     *reinterpret_cast<intx4*>(X + xoff<P, NQ>(pe_slot, pe_t, 2 * QS)) = *reinterpret_cast<const intx4*>(pe2);
+#pragma unroll
+    for (int q = 2 * QS + 1; q < NQ; ++q)
+      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(pe_slot, pe_t, q)) = intx4{0, 0, 0, 0};
   }
   Real pf = 1;
   if (inl) {
@@ -1339,12 +1341,14 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
     pf = nact - (Real)1;
     pf = pf > (Real)0 ? (Real)1 / pf : (Real)1;
   }
+  // LDS offsets of this thread's a / s chunks in image row r0 (+ RG i rows per iteration)
+  const int oa = xoff<P, NQ>(r0, tk, qk), os = xoff<P, NQ>(r0, tk, QS + qk);
 #pragma unroll
   for (int i = 0; i < PV; ++i) {
-    const unsigned c = threadIdx.x + 512u * i;
-    if (c < NV) {
-      const int pair = c / QS, q = c % QS;
-      const int slot = slot_lo + pair / kT, tt = pair % kT;
+    const int r = r0 + RG * i;
+    if (lane_on && r < R0) {
+      const int rr = r - slot_lo;
+      const bool in = rr >= 0 && rr < nrow;
       intx4 out = va[i][0];
       if (inl) {
         // a_u = p * sum of the other users' act*sp (packed f16 adds in the f16 policy; one
@@ -1369,8 +1373,8 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
           out = *reinterpret_cast<const intx4*>(o);
         }
       }
-      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(slot, tt, q)) = out;
-      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(slot, tt, QS + q)) = vs[i];
+      *reinterpret_cast<intx4*>(X + oa + RG * i * slot_pitch<P>()) = in ? out : intx4{0, 0, 0, 0};
+      *reinterpret_cast<intx4*>(X + os + RG * i * slot_pitch<P>()) = in ? vs[i] : intx4{0, 0, 0, 0};
     }
   }
   stamp(26);
@@ -1481,6 +1485,7 @@ __global__ __launch_bounds__(512) void k_update(BlockParams<P> prm) {
 }
 
 // ======================================================================= launchers
+
 template <class P>
 struct Launch {
   using A = FwdArgs<typename P::WT, typename P::BT, typename P::S>;
