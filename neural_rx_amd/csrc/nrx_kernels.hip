@@ -10,11 +10,13 @@
 //               in its prologue (slot_norm)
 //               one launch per init head m, accumulating the Var-IO mcs mix
 //               (neural_rx.py:562-569); the last one runs the aggregation MLP of
-//               iteration 0 in its conv3 epilogue and the leave-one-out user combine
-//               in a last-arriver tail                            (neural_rx.py:135-207)
+//               iteration 0 in its conv3 epilogue and stores act_u * sp_u
 //   k_update    z=[a,s,pe] -> 3 separable convs + skip           (copy_pytorch.py:267-287)
-//               epilogue: next iteration's aggregation MLP + tail, or after the last
+//               z-load forms the leave-one-out user mean from the act * sp rows
+//               (neural_rx.py:135-207; U <= 2: LDS-DMA copy, U <= 4: register sum);
+//               epilogue: next iteration's aggregation MLP, or after the last
 //               iteration the LLR head(s) + ChEst head           (neural_rx.py:309-404)
+//   k_combine   U > 4 only: the leave-one-out mean as its own pass
 //
 // Tiling.  The resource grid of one (slot, user) is an F x 16 image (T = 14 padded to 16
 // with zero rows).  One MFMA tile = one subcarrier row: 16 symbols x 16 output channels.
@@ -596,9 +598,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 // 16-channel tile (lane (t, g) holds channels 16 n + P::co(g, j)) is reused as the B
 // operand of the next MFMA, with that layer's K axis permuted on the host to match
 // (nrx_api.cpp, kperm_*).  After an update that is not the last, the epilogue applies
-// the aggregation MLP of the next iteration and stores act_u * sp_u; the last workgroup
-// of each (slot, strip) to arrive then forms the leave-one-out mean for all users.  After
-// the last update the epilogue runs the LLR / ChEst readouts instead.
+// the aggregation MLP of the next iteration and stores act_u * sp_u; the next launch's
+// z-load (or k_combine for U > 4) forms the leave-one-out mean.  After the last update the
+// epilogue runs the LLR / ChEst readouts instead.
 //
 // State / aggregate buffers are compact: [B][U][F][14][56] (no padding in HBM).
 
@@ -1250,6 +1252,55 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
   stamp(4);
 }
 
+// 16 zero bytes: the LDS-DMA source of every z chunk that is zero (pad symbols, rows
+// outside the grid, channel padding, the missing other user of U = 1)
+__device__ intx4 g_zero16[1];
+
+#ifndef NRX_ZDMA
+#define NRX_ZDMA 1
+#endif
+
+// f16 update z-load for U <= 2 as LDS-DMA (global_load_lds_dwordx4): with at most one
+// other user the leave-one-out mean is a plain copy of that user's act*sp plane (p = 1 for
+// any activity pattern of two users), so every 16-byte chunk of the z image is a copy of
+// one global chunk or zero, and the image is filled with no VGPR round trip and no LDS
+// store instructions.  One wave-instruction fills 1 KB of LDS linearly (4 symbols x 16
+// chunks of one slot); the chunk swizzle is applied on the source address (the lane at
+// physical chunk q' of symbol t loads logical chunk q' ^ swz(t)).  The pe chunk (2 values)
+// is written by ds_write after the DMA has landed.
+template <class P>
+__device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X, int b, int u, int f_start) {
+  using S = typename P::S;
+  static_assert(sizeof(S) == 2 && kUPD_CINP * 2 / 16 == 16, "f16 z image with 16 chunks per symbol row");
+  constexpr int R0 = strip_slots<P>();
+  constexpr int QS = kDS / P::EPC;   // 7 chunks of a, then 7 of s
+  const auto& a = prm.a;
+  const int F = a.F, U = a.U;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tq = lane >> 4, qp = lane & 15;
+  const S* sp = a.s_in + srow(b, u, 0, 0, U, F);
+  const S* ap = a.a + srow(b, U == 2 ? 1 - u : 0, 0, 0, U, F);
+  const bool has_a = U == 2;
+  typedef __attribute__((address_space(3))) void lds_void;
+  typedef const __attribute__((address_space(1))) void glb_void;
+  for (int k = wave; k < R0 * 4; k += 8) {
+    const int r = k >> 2, t = 4 * (k & 3) + tq;
+    const int f = f_start + r;
+    const int q = qp ^ swz<16>(t);
+    const S* src = reinterpret_cast<const S*>(g_zero16);
+    if (t < kT && f >= 0 && f < F) {
+      const int re = (f * kT + t) * kDS;
+      if (q < QS) {
+        if (has_a) src = ap + re + P::EPC * q;
+      } else if (q < 2 * QS) {
+        src = sp + re + P::EPC * (q - QS);
+      }
+    }
+    __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(X + k * 1024), 16, 0, 0);
+  }
+}
+
 // UpdateState of user u on the strip (z = [a, s, pe]).
 template <class P, int CHP, int TAILM>
 __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* smem, int b, int u, int strip) {
@@ -1263,6 +1314,36 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
   const int f_start = f0 - kHalo;
   char* X = smem;
   char* WB = smem + R0 * slot_pitch<P>();
+  if constexpr (sizeof(S) == 2 && NRX_ZDMA != 0) {
+    if (prm.inline_combine && U <= 2) {
+      SepStage<kUPD_CINP, kHID> w1;
+      w1.load(prm.w[0]);
+      zload_dma_u2<P>(prm, X, b, u, f_start);
+      const int pe_slot = threadIdx.x / kT, pe_t = threadIdx.x % kT;
+      const int pe_f = f_start + pe_slot;
+      const bool pe_ok = pe_slot < R0 && pe_f >= 0 && pe_f < F;
+      const float2 pe_v = *reinterpret_cast<const float2*>(
+          a.pe + (((size_t)u * F + (pe_ok ? pe_f : 0)) * kT + (pe_ok ? pe_t : 0)) * 2);
+      stamp(24);
+      stamp(25);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();   // every wave's DMA has landed: the pe chunks may be overwritten
+      stamp(26);
+      if (pe_slot < R0) {
+        S pe2[P::EPC] = {};
+        pe2[0] = pe_ok ? (S)pe_v.x : (S)0;
+        pe2[1] = pe_ok ? (S)pe_v.y : (S)0;
+        *reinterpret_cast<intx4*>(X + xoff<P, NQ>(pe_slot, pe_t, 2 * QS)) = *reinterpret_cast<const intx4*>(pe2);
+      }
+      w1.store(WB);
+      stamp(27);
+      __syncthreads();
+      stamp(1);
+      strip_block<P, kUPD_CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 0, 0, false);
+      stamp(4);
+      return;
+    }
+  }
   // z chunks: [0,QS) <- a, [QS,2QS) <- s, 2QS <- pe (2 values), rest 0.
   // a_u = (sum_u' sp_u' - sp_u) * p is formed here from the producer's act*sp rows when
   // U <= kInlineUsers (AggregateUserStates' leave-one-out mean, neural_rx.py:191-204);
