@@ -997,6 +997,17 @@ struct EpiConv3 {
               const int f = f_start + p0 + r0 + r;
               float* dst = a.llr + ((((size_t)hh * a.B + b) * U + u) * F + f) * kT * a.bits_max + t * a.bits_max;
               // head bits beyond head_bits[hh] (masking: sliced later) are written as 0
+              if constexpr (sizeof(S) == 2) {
+                if (a.bits_max == 4) {
+                  // 16-QAM: lanes g = 0 hold the 4 LLRs of their symbol, one 16-byte store
+                  const int nb = a.head_bits[hh];
+                  if (g == 0)
+                    *reinterpret_cast<floatx4*>(dst) =
+                        floatx4{nb > 0 ? (float)o[r][0][0] : 0.f, nb > 1 ? (float)o[r][0][1] : 0.f,
+                                nb > 2 ? (float)o[r][0][2] : 0.f, nb > 3 ? (float)o[r][0][3] : 0.f};
+                  continue;
+                }
+              }
 #pragma unroll
               for (int j = 0; j < 4; ++j) {
                 const int co = P::co(g, j);
@@ -1132,12 +1143,21 @@ constexpr int init_cinp(int kc) {
 // given (F x 14 x 2A floats, nq float4s), divide-no-nan (an all-zero slot gets 0).  Every
 // workgroup of the slot computes it (21 KB at nrx_rt, L2-resident after the first): no
 // separate launch.  Double accumulation; `red` is 8 doubles of LDS.
+// acc + v.v as an explicit fma chain: the contraction is fixed in the source, so the slot norm
+// (and with it every later rounding of the slot) does not move with the surrounding codegen
+__device__ __forceinline__ double sq4(double acc, floatx4 v) {
+  acc = __builtin_fma((double)v[0], (double)v[0], acc);
+  acc = __builtin_fma((double)v[1], (double)v[1], acc);
+  acc = __builtin_fma((double)v[2], (double)v[2], acc);
+  return __builtin_fma((double)v[3], (double)v[3], acc);
+}
+
 __device__ __forceinline__ double slot_norm(const float* y, int nq, double* red) {
   const floatx4* yq = reinterpret_cast<const floatx4*>(y);
   double acc = 0.0;
   for (int i = threadIdx.x; i < nq; i += 512) {
     const floatx4 v = yq[i];
-    acc += (double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2] + (double)v[3] * v[3];
+    acc = sq4(acc, v);
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
@@ -1158,7 +1178,7 @@ __global__ __launch_bounds__(1024) void k_norm(const float* __restrict__ y, int 
   double acc = 0.0;
   for (int i = threadIdx.x; i < nq; i += 1024) {
     const floatx4 v = yq[i];
-    acc += (double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2] + (double)v[3] * v[3];
+    acc = sq4(acc, v);
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
@@ -1207,23 +1227,57 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
     const int f = f_start + lf;
     const bool ok = lf < R0 && tt < kT && f >= 0 && f < F;
     float yv[A2P], hv[A2P];
-    float2 pv = {0.f, 0.f};
     const size_t re = ((size_t)b * F + (ok ? f : 0)) * kT + (ok ? tt : 0);
-    const float2* yp = reinterpret_cast<const float2*>(a.y + re * A2);
-    const float2* hp = reinterpret_cast<const float2*>(a.h_hat + (((size_t)b * U + u) * F * kT + (re - (size_t)b * F * kT)) * A2);
+    const float* yp = a.y + re * A2;
+    const float* hp = a.h_hat + (((size_t)b * U + u) * F * kT + (re - (size_t)b * F * kT)) * A2;
+    // every load unconditional from a clamped address (row 0 / last pair of the row) and
+    // masked afterwards: a load under a per-element runtime condition makes the compiler
+    // branch around it and wait for each one in turn.  16-byte loads when 2A % 4 == 0.
+    if ((A2 & 3) == 0) {
+      const int nk = A2 / 4;
+      float4 yl[A2P / 4], hl[A2P / 4];
 #pragma unroll
-    for (int k = 0; k < A2P / 2; ++k) {
-      float2 v = {0.f, 0.f}, w = {0.f, 0.f};
-      if (ok && 2 * k < A2) {
-        v = yp[k];
-        if (a.use_h) w = hp[k];
+      for (int k = 0; k < A2P / 4; ++k) yl[k] = reinterpret_cast<const float4*>(yp)[k < nk ? k : nk - 1];
+#pragma unroll
+      for (int k = 0; k < A2P / 4; ++k) hl[k] = float4{0.f, 0.f, 0.f, 0.f};
+      if (a.use_h) {
+#pragma unroll
+        for (int k = 0; k < A2P / 4; ++k) hl[k] = reinterpret_cast<const float4*>(hp)[k < nk ? k : nk - 1];
       }
-      yv[2 * k] = v.x;
-      yv[2 * k + 1] = v.y;
-      hv[2 * k] = w.x;
-      hv[2 * k + 1] = w.y;
+#pragma unroll
+      for (int k = 0; k < A2P / 4; ++k) {
+        const bool on = ok && k < nk;
+        yv[4 * k] = on ? yl[k].x : 0.f;
+        yv[4 * k + 1] = on ? yl[k].y : 0.f;
+        yv[4 * k + 2] = on ? yl[k].z : 0.f;
+        yv[4 * k + 3] = on ? yl[k].w : 0.f;
+        hv[4 * k] = on ? hl[k].x : 0.f;
+        hv[4 * k + 1] = on ? hl[k].y : 0.f;
+        hv[4 * k + 2] = on ? hl[k].z : 0.f;
+        hv[4 * k + 3] = on ? hl[k].w : 0.f;
+      }
+    } else {
+      const int nk = A2 / 2;
+      float2 yl[A2P / 2], hl[A2P / 2];
+#pragma unroll
+      for (int k = 0; k < A2P / 2; ++k) yl[k] = reinterpret_cast<const float2*>(yp)[k < nk ? k : nk - 1];
+#pragma unroll
+      for (int k = 0; k < A2P / 2; ++k) hl[k] = float2{0.f, 0.f};
+      if (a.use_h) {
+#pragma unroll
+        for (int k = 0; k < A2P / 2; ++k) hl[k] = reinterpret_cast<const float2*>(hp)[k < nk ? k : nk - 1];
+      }
+#pragma unroll
+      for (int k = 0; k < A2P / 2; ++k) {
+        const bool on = ok && k < nk;
+        yv[2 * k] = on ? yl[k].x : 0.f;
+        yv[2 * k + 1] = on ? yl[k].y : 0.f;
+        hv[2 * k] = on ? hl[k].x : 0.f;
+        hv[2 * k + 1] = on ? hl[k].y : 0.f;
+      }
     }
-    if (ok) pv = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + f) * kT + tt) * 2);
+    float2 pv = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + (ok ? f : 0)) * kT + (ok ? tt : 0)) * 2);
+    if (!ok) pv = float2{0.f, 0.f};
     // large grids: the per-slot k_norm pass already reduced y (every workgroup of the slot
     // re-reading the whole grid costs O(strips x grid) there); small grids: fused here
     const Real ns = prm.norm_pre ? (Real)a.norm[b] : (Real)slot_norm(a.y + (size_t)b * F * kT * A2, F * kT * A2 / 4, red);
