@@ -431,6 +431,17 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
   if constexpr (E::kNoBarrier) {
     // the epilogue neither writes LDS nor reads anything staged after the math: each
     // wave runs it as soon as its own math is done (post_math is empty for these)
+    if constexpr (E::kNextHook) {
+      if (epi.nb >= 0) {
+        // paired items: once every wave is past its conv3 reads the strip image is free,
+        // and the next item's z image is DMA'd into it while this epilogue runs.  The
+        // epilogue's own global loads are settled first (a use of a load result behind
+        // an LDS-DMA would wait for the DMA too).
+        if (act) epi.template settle<R>(pf);
+        __syncthreads();
+        epi.next_hook();
+      }
+    }
     if (act) epi.template run<R>(acc, pf, p0, t, g, 0, R);
     stamp(12 + 5 * in_off);
   } else {
@@ -484,6 +495,7 @@ struct EpiInPlace {
   template <int R>
   using PrefT = NoPref;
   static constexpr bool kNoBarrier = false;
+  static constexpr bool kNextHook = false;
   static constexpr int kEarlyRow = 2;
   char* X;
   int in_off, pos_hi, f_start, F;
@@ -619,6 +631,7 @@ struct BlockParams {
   int order_rev;                                         // XCD-local work order reversed
   int inline_combine;                                    // U <= kInlineUsers: z-load forms a
   int norm_pre;                                          // a.norm[b] holds the slot norm (k_norm ran)
+  int pair;                                              // k_update: two items per workgroup (2nd prefetched)
 };
 
 template <class P>
@@ -757,6 +770,7 @@ struct EpiConv3 {
   };
   // no LDS writes; the readout tail reads head weights staged into X after the math
   static constexpr bool kNoBarrier = TAILM != TAIL_READOUT;
+  static constexpr bool kNextHook = TAILM == TAIL_AGG && P::WLDS;
   static constexpr int kEarlyRow = 8;      // readout: every row after the barrier
   const BlockParams<P>* prm;
   char* X;
@@ -765,6 +779,20 @@ struct EpiConv3 {
   int b, u, f_start, pos_hi, mode;   // mode 0: update (+skip), 1: init (x wm, Var-IO accumulate)
   Real wm;
   bool first;
+  Real act_h;             // active[b][u], loaded before the conv3 math
+  int nb, nu, nfs;        // paired k_update: next item (nb < 0: none)
+
+  template <int R>
+  __device__ void settle(PrefT<R>& pf) {
+    if constexpr (sizeof(S) == 2) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int n = 0; n < NTS; ++n) asm volatile("" : "+v"(pf.prev[r][n]));
+    }
+    asm volatile("" : "+v"(act_h));
+  }
+  __device__ void next_hook() const;
 
   __device__ bool row_ok(int p, int t) const { return p < pos_hi && f_start + p < prm->a.F && t < kT; }
 
@@ -928,7 +956,7 @@ struct EpiConv3 {
     if constexpr (TAILM == TAIL_AGG) {
       // sp_u = act_u * (W2 relu(W1 s + b1) + b2)  -> a_out (combined by the tail)
       Real hdn[R][kAGG / 16][4], sp[R][NTS][4];
-      const Real act = (Real)a.active[(size_t)b * U + u];
+      const Real act = act_h;
       CFrag<P, kAGG / 16> hb[R];
       if constexpr ((NRX_ABLATE & 128) != 0 && P::WLDS) {
 #pragma unroll
@@ -1051,7 +1079,8 @@ constexpr bool kPrefetchW = NRX_PREFETCH_W != 0;
 // aggregation MLP) are issued before its math and stored to WB after it.
 template <class P, int CINP, int CHP, int TAILM>
 __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, char* WB, int b, int u,
-                                            int f_start, int mode, typename P::Real wm, bool first) {
+                                            int f_start, int mode, typename P::Real wm, bool first, int nb = -1,
+                                            int nu = 0, int nfs = 0) {
   constexpr int R0 = strip_slots<P>();
   const int F = prm.a.F;
   {
@@ -1111,7 +1140,9 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
     };
     if constexpr (P::WLDS && TAILM == TAIL_READOUT && kPrefetchW) ld();
     run_layer<P, kHID, kDSP>(X, WB, prm.w[2], 2, kHalo, R0 - kHalo, [&](auto ws) {
-      return EpiConv3<P, decltype(ws), CHP, TAILM>{&prm, X, WB, ws, b, u, f_start, R0 - kHalo, mode, wm, first};
+      return EpiConv3<P, decltype(ws), CHP, TAILM>{&prm, X, WB, ws, b, u, f_start, R0 - kHalo, mode, wm, first,
+                                                   (typename P::Real)prm.a.active[(size_t)b * prm.a.U + u],
+                                                   nb, nu, nfs};
     }, [&]() {
       if constexpr (P::WLDS && TAILM == TAIL_READOUT) {
         if constexpr (!kPrefetchW) ld();
@@ -1355,6 +1386,68 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
   }
 }
 
+template <class P, class WS, int CHP, int TAILM>
+__device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook() const {
+  if constexpr (kNextHook) zload_dma_u2<P>(*prm, X, nb, nu, nfs);
+}
+
+// Rest of an update item whose z image is being filled by LDS-DMA (issued by the caller, or
+// by the previous item's conv3 hook): conv1 weights, pe chunk once the DMA has landed, the
+// block.  (nb, nu, nfs): the next item of a paired workgroup (nb < 0: none).
+template <class P, int CHP, int TAILM>
+__device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X, char* WB, int b, int u, int f_start,
+                                             int nb, int nu, int nfs) {
+  using S = typename P::S;
+  constexpr int R0 = strip_slots<P>();
+  constexpr int NQ = kUPD_CINP * (int)sizeof(S) / 16;
+  constexpr int QS = kDS / P::EPC;
+  const auto& a = prm.a;
+  const int F = a.F;
+  SepStage<kUPD_CINP, kHID> w1;
+  w1.load(prm.w[0]);
+  const int pe_slot = threadIdx.x / kT, pe_t = threadIdx.x % kT;
+  const int pe_f = f_start + pe_slot;
+  const bool pe_ok = pe_slot < R0 && pe_f >= 0 && pe_f < F;
+  const float2 pe_v = *reinterpret_cast<const float2*>(
+      a.pe + (((size_t)u * F + (pe_ok ? pe_f : 0)) * kT + (pe_ok ? pe_t : 0)) * 2);
+  stamp(24);
+  stamp(25);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();   // every wave's DMA has landed (and a previous item's epilogue is done)
+  stamp(26);
+  if (pe_slot < R0) {
+    S pe2[P::EPC] = {};
+    pe2[0] = pe_ok ? (S)pe_v.x : (S)0;
+    pe2[1] = pe_ok ? (S)pe_v.y : (S)0;
+    *reinterpret_cast<intx4*>(X + xoff<P, NQ>(pe_slot, pe_t, 2 * QS)) = *reinterpret_cast<const intx4*>(pe2);
+  }
+  w1.store(WB);
+  stamp(27);
+  __syncthreads();
+  stamp(1);
+  strip_block<P, kUPD_CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 0, 0, false, nb, nu, nfs);
+  stamp(4);
+}
+
+#ifndef NRX_PAIR
+#define NRX_PAIR 1
+#endif
+
+// Two update items (aggregation tail) per workgroup: item 1's z image is DMA'd into the
+// strip image during item 0's epilogue (EpiConv3::next_hook), so its load overlaps that
+// epilogue instead of stalling a chip-wide load phase of its own.
+template <class P, int CHP>
+__device__ __forceinline__ void update_pair(const BlockParams<P>& prm, char* smem, int b0, int u0, int s0, int b1,
+                                            int u1, int s1) {
+  constexpr int R0 = strip_slots<P>();
+  char* X = smem;
+  char* WB = smem + R0 * slot_pitch<P>();
+  const int fs0 = s0 * P::FO - kHalo, fs1 = s1 * P::FO - kHalo;
+  zload_dma_u2<P>(prm, X, b0, u0, fs0);
+  dma_item_run<P, CHP, TAIL_AGG>(prm, X, WB, b0, u0, fs0, b1, u1, fs1);
+  dma_item_run<P, CHP, TAIL_AGG>(prm, X, WB, b1, u1, fs1, -1, 0, 0);
+}
+
 // UpdateState of user u on the strip (z = [a, s, pe]).
 template <class P, int CHP, int TAILM>
 __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* smem, int b, int u, int strip) {
@@ -1370,31 +1463,8 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
   char* WB = smem + R0 * slot_pitch<P>();
   if constexpr (sizeof(S) == 2 && NRX_ZDMA != 0) {
     if (prm.inline_combine && U <= 2) {
-      SepStage<kUPD_CINP, kHID> w1;
-      w1.load(prm.w[0]);
       zload_dma_u2<P>(prm, X, b, u, f_start);
-      const int pe_slot = threadIdx.x / kT, pe_t = threadIdx.x % kT;
-      const int pe_f = f_start + pe_slot;
-      const bool pe_ok = pe_slot < R0 && pe_f >= 0 && pe_f < F;
-      const float2 pe_v = *reinterpret_cast<const float2*>(
-          a.pe + (((size_t)u * F + (pe_ok ? pe_f : 0)) * kT + (pe_ok ? pe_t : 0)) * 2);
-      stamp(24);
-      stamp(25);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();   // every wave's DMA has landed: the pe chunks may be overwritten
-      stamp(26);
-      if (pe_slot < R0) {
-        S pe2[P::EPC] = {};
-        pe2[0] = pe_ok ? (S)pe_v.x : (S)0;
-        pe2[1] = pe_ok ? (S)pe_v.y : (S)0;
-        *reinterpret_cast<intx4*>(X + xoff<P, NQ>(pe_slot, pe_t, 2 * QS)) = *reinterpret_cast<const intx4*>(pe2);
-      }
-      w1.store(WB);
-      stamp(27);
-      __syncthreads();
-      stamp(1);
-      strip_block<P, kUPD_CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 0, 0, false);
-      stamp(4);
+      dma_item_run<P, CHP, TAILM>(prm, X, WB, b, u, f_start, -1, 0, 0);
       return;
     }
   }
@@ -1615,6 +1685,15 @@ __global__ __launch_bounds__(512) void k_update(BlockParams<P> prm) {
   int b, u, strip;
   work_item(blockIdx.x, prm.a.B, prm.a.U, prm.strips, prm.order_rev, b, u, strip);
   stamp(0);
+  if constexpr (TAILM == TAIL_AGG && P::WLDS && NRX_PAIR != 0 && NRX_ZDMA != 0) {
+    if (prm.pair) {
+      int b1, u1, s1;
+      work_item(blockIdx.x + gridDim.x, prm.a.B, prm.a.U, prm.strips, prm.order_rev, b1, u1, s1);
+      update_pair<P, CHP>(prm, smem, b, u, strip, b1, u1, s1);
+      stamp(5);
+      return;
+    }
+  }
   update_user<P, CHP, TAILM>(prm, smem, b, u, strip);
   stamp(5);
 }
@@ -1661,6 +1740,7 @@ struct Launch {
     BlockParams<P> bp;
     bp.a = args;
     bp.inline_combine = args.U <= kInlineUsers;
+    bp.pair = 0;
     bp.strips = strips;
     const int nq = args.F * kT * 2 * args.A / 4;
     bp.norm_pre = nq > kNormFusedMaxQ;
@@ -1732,8 +1812,15 @@ struct Launch {
         if (ch32) k_update<P, 32, TAIL_READOUT><<<grid, 512, L, st>>>(bp);
         else k_update<P, 16, TAIL_READOUT><<<grid, 512, L, st>>>(bp);
       } else {
-        if (ch32) k_update<P, 32, TAIL_AGG><<<grid, 512, L, st>>>(bp);
-        else k_update<P, 16, TAIL_AGG><<<grid, 512, L, st>>>(bp);
+        // two items per workgroup when there are at least two per CU (256 CUs) and the
+        // halves keep the XCD grouping of work_item (items % 16 == 0)
+        const int items = (int)grid.x;
+        bp.pair = P::WLDS && NRX_PAIR != 0 && NRX_ZDMA != 0 && args.U <= 2 && bp.inline_combine &&
+                  items % 16 == 0 && items >= 512;
+        const dim3 g2(bp.pair ? items / 2 : items);
+        if (ch32) k_update<P, 32, TAIL_AGG><<<g2, 512, L, st>>>(bp);
+        else k_update<P, 16, TAIL_AGG><<<g2, 512, L, st>>>(bp);
+        bp.pair = 0;
       }
       E_(K_UPDATE);
       if (!last) combine(bp.a.a_out);
