@@ -141,3 +141,20 @@ def test_receiver_layouts_consistent():
                                atol=1e-5)
     ref = run_oracle(case)
     assert np.abs(llr_s.cpu().numpy() - ref["llr"][0]).max() < F32X_LLR_TOL
+
+
+def test_batch_composition_invariance_paired_items():
+    # B = 128, U = 2 launches the paired update path (two items per workgroup, the second
+    # item's z image DMA'd during the first one's epilogue); a slot's outputs must not depend
+    # on the batch it runs in or on which workgroup ran it: bit-identical to a B = 4 run
+    import torch
+    case = make_case("nrx_rt", batch=128, users=2, prbs=4, snr_db=12, seed=11)
+    eng = engine_for(case)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda()
+    llr, h = eng.forward(t(case.y), t(case.pe), t(case.h_hat), t(case.active), None, None, "f16")
+    sel = [0, 5, 77, 127]
+    llr4, h4 = eng.forward(t(case.y[sel]), t(case.pe), t(case.h_hat[sel]), t(case.active[sel]), None, None, "f16")
+    torch.cuda.synchronize()
+    assert np.array_equal(llr.cpu().numpy()[:, sel], llr4.cpu().numpy())
+    assert np.array_equal(h.cpu().numpy()[sel], h4.cpu().numpy())
+    assert np.isfinite(llr.cpu().numpy()).all()
