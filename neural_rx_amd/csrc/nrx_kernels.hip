@@ -432,12 +432,16 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
     // the epilogue neither writes LDS nor reads anything staged after the math: each
     // wave runs it as soon as its own math is done (post_math is empty for these)
     if constexpr (E::kNextHook) {
+      // outside the nb test too: the waitcnt pass joins the paths after it
+      epi.template settle<R>(pf);
       if (epi.nb >= 0) {
         // paired items: once every wave is past its conv3 reads the strip image is free,
         // and the next item's z image is DMA'd into it while this epilogue runs.  The
         // epilogue's own global loads are settled first (a use of a load result behind
-        // an LDS-DMA would wait for the DMA too).
-        if (act) epi.template settle<R>(pf);
+        // an LDS-DMA would wait for the DMA too).  Settled on every wave, not only under
+        // `act`: the waitcnt pass merges the pending-load state of both paths, so a
+        // conditional settle left the skip-row loads pending and the first use in the
+        // epilogue waited for vmcnt(0), i.e. for the whole DMA.
         __syncthreads();
         epi.next_hook();
       }
@@ -1700,6 +1704,16 @@ __global__ __launch_bounds__(512) void k_update(BlockParams<P> prm) {
 
 // ======================================================================= launchers
 
+// CUs per device, recorded by setup_kernels() (nrx_create) for the pairing heuristic;
+// 256 (MI355X) until then
+constexpr int kMaxDevices = 64;
+static int g_cu_count[kMaxDevices];
+static int cu_count() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices || g_cu_count[dev] <= 0) return 256;
+  return g_cu_count[dev];
+}
+
 template <class P>
 struct Launch {
   using A = FwdArgs<typename P::WT, typename P::BT, typename P::S>;
@@ -1812,11 +1826,12 @@ struct Launch {
         if (ch32) k_update<P, 32, TAIL_READOUT><<<grid, 512, L, st>>>(bp);
         else k_update<P, 16, TAIL_READOUT><<<grid, 512, L, st>>>(bp);
       } else {
-        // two items per workgroup when there are at least two per CU (256 CUs) and the
-        // halves keep the XCD grouping of work_item (items % 16 == 0)
+        // two items per workgroup when there are at least two per CU (CU count of the
+        // device, one workgroup per CU by LDS) and the halves keep the XCD grouping of
+        // work_item (items % 16 == 0)
         const int items = (int)grid.x;
         bp.pair = P::WLDS && NRX_PAIR != 0 && NRX_ZDMA != 0 && args.U <= 2 && bp.inline_combine &&
-                  items % 16 == 0 && items >= 512;
+                  items % 16 == 0 && items >= 2 * cu_count();
         const dim3 g2(bp.pair ? items / 2 : items);
         if (ch32) k_update<P, 32, TAIL_AGG><<<g2, 512, L, st>>>(bp);
         else k_update<P, 16, TAIL_AGG><<<g2, 512, L, st>>>(bp);
@@ -1842,6 +1857,11 @@ hipError_t launch_forward_f64(const FwdArgs<double, double, float>& args,
 }
 
 hipError_t setup_kernels() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0 &&
+      dev >= 0 && dev < kMaxDevices)
+    g_cu_count[dev] = cus;
   hipError_t e = Launch<P16>::setup();
   hipError_t e2 = Launch<P64>::setup();
   return e != hipSuccess ? e : e2;

@@ -143,16 +143,35 @@ def test_receiver_layouts_consistent():
     assert np.abs(llr_s.cpu().numpy() - ref["llr"][0]).max() < F32X_LLR_TOL
 
 
-def test_batch_composition_invariance_paired_items():
-    # B = 128, U = 2 launches the paired update path (two items per workgroup, the second
-    # item's z image DMA'd during the first one's epilogue); a slot's outputs must not depend
-    # on the batch it runs in or on which workgroup ran it: bit-identical to a B = 4 run
+# Paired update path (two aggregation-tail items per workgroup, the second item's z image
+# DMA'd during the first one's epilogue; taken when items % 16 == 0 and items >= 2 x CUs).
+# Each case is compared bit for bit with an unpaired run of a few of its slots (small B: one
+# item per workgroup): a slot's outputs must not depend on the batch it runs in or on which
+# workgroup ran it.  Cases: the bench shape; U = 1 (no other user: zero aggregate chunks);
+# a random active mask (act = 0 users, p = 1 / (#active - 1)); B = 136 (not a multiple of 8:
+# work_item's plain-order tail); F = 60 (a partial last strip, 3 strips).
+PAIRED_CASES = {
+    "bench_b128_u2": dict(batch=128, users=2, prbs=4),
+    "u1_b512": dict(batch=512, users=1, prbs=4),
+    "random_active_b128": dict(batch=128, users=2, prbs=4, active="random"),
+    "b136_tail": dict(batch=136, users=2, prbs=4),
+    "f60_partial_strip": dict(batch=128, users=2, prbs=5),
+}
+
+
+@pytest.mark.parametrize("name", list(PAIRED_CASES))
+def test_batch_composition_invariance_paired_items(name):
     import torch
-    case = make_case("nrx_rt", batch=128, users=2, prbs=4, snr_db=12, seed=11)
+    kw = dict(PAIRED_CASES[name])
+    rng = np.random.default_rng(5)
+    if kw.get("active") == "random":
+        kw["active"] = (rng.random((kw["batch"], kw["users"])) < 0.6).astype(np.float32)
+    case = make_case("nrx_rt", snr_db=12, seed=11, **kw)
     eng = engine_for(case)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda()
     llr, h = eng.forward(t(case.y), t(case.pe), t(case.h_hat), t(case.active), None, None, "f16")
-    sel = [0, 5, 77, 127]
+    B = kw["batch"]
+    sel = [0, 5, 77, B - 1]
     llr4, h4 = eng.forward(t(case.y[sel]), t(case.pe), t(case.h_hat[sel]), t(case.active[sel]), None, None, "f16")
     torch.cuda.synchronize()
     assert np.array_equal(llr.cpu().numpy()[:, sel], llr4.cpu().numpy())

@@ -2,9 +2,10 @@
 import ctypes, os, sys, subprocess
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                "-DNRX_STAMPS", "neural_rx_amd/csrc/nrx_kernels.hip", "neural_rx_amd/csrc/nrx_api.cpp",
-                "-o", "/tmp/libnrx_stamps.so"], check=True)
+from neural_rx_amd import build as _B
+if not os.path.exists("/tmp/libnrx_stamps.so"):
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                    "-DNRX_STAMPS", *_B.SOURCES, "-o", "/tmp/libnrx_stamps.so"], check=True)
 import torch
 from neural_rx_amd import _lib
 lib = _lib.load("/tmp/libnrx_stamps.so")
@@ -18,8 +19,9 @@ sl = synth.generate(B, U, prbs, 4, [4, 4], (0, 1), snr_db=10, seed=3)
 eng = CGNNEngine(spec, W.load("nrx_rt"))
 t = lambda a: torch.from_numpy(a).cuda()
 pe = t(compute_pe(U, 48, (2, 11), (0, 1)))
-for _ in range(5):
-    eng.forward(t(sl.y), pe, t(sl.h_hat), t(sl.active), None, 2, "f16")
+dy, dh, da = t(sl.y), t(sl.h_hat), t(sl.active)
+for _ in range(300):
+    eng.forward(dy, pe, dh, da, None, 2, "f16")
 torch.cuda.synchronize()
 n = 512
 buf = np.zeros((n, 32), np.uint64)
