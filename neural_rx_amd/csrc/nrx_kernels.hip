@@ -52,7 +52,7 @@ namespace nrx {
 
 #ifdef NRX_STAMPS
 // diagnostic builds only: s_memtime per phase, wave 0 lane 0 of each workgroup
-__device__ unsigned long long g_nrx_stamps[4096][32];
+__device__ unsigned long long g_nrx_stamps[4096][64];
 // set by the host for the k_update launch to record; __constant__ so that the flag is a
 // scalar (SMEM) load and a stamp does not wait for the wave's outstanding vector loads
 __constant__ int g_nrx_stamp_on;
@@ -266,6 +266,18 @@ struct WLds {
   __device__ typename P::DV dwv(int tap, int kc, int g) const {
     return *reinterpret_cast<const half8*>(base + kWPw + (tap * CINP + kc * 32 + g * 8) * 2);
   }
+  // the 9 taps of chunk kc from one opaque base register: the image sits ~155 KB into LDS,
+  // beyond the 16-bit ds_read offset, so with a foldable base the compiler emits one v_add
+  // per tap; hidden, every tap is an immediate offset (tap * CINP * 2 <= 2 KB)
+  __device__ void dw_taps(int kc, int g, typename P::DV (&w)[9]) const {
+    typedef const __attribute__((address_space(3))) char lds_char;
+    typedef const __attribute__((address_space(3))) half8 lds_half8;
+    unsigned p = (unsigned)(size_t)(lds_char*)(base + kWPw) + (unsigned)((kc * 32 + g * 8) * 2);
+    asm volatile("" : "+v"(p));
+    lds_char* q = (lds_char*)(size_t)p;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) w[k] = *reinterpret_cast<lds_half8*>(q + k * CINP * 2);
+  }
   __device__ typename P::Acc bias_acc(int n, int g) const {
     return P::bias_acc(reinterpret_cast<const float*>(base + kWBias), n, g);
   }
@@ -279,6 +291,10 @@ struct WGlb {
   }
   __device__ typename P::DV dwv(int tap, int kc, int g) const {
     return P::ld_w(w.dw + tap * CINP + kc * P::KC + g * P::CPL);
+  }
+  __device__ void dw_taps(int kc, int g, typename P::DV (&w9)[9]) const {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) w9[k] = dwv(k, kc, g);
   }
   __device__ typename P::Acc bias_acc(int n, int g) const { return P::bias_acc(w.b, n, g); }
 };
@@ -360,27 +376,32 @@ template <class P, int CINP, int COUTP, bool FIRST, int R, class WS>
 __device__ __forceinline__ void conv_chunk(const char* X, const int (&rb)[R + 2], int sw, int kc, int g,
                                            int lane, const WS& ws, typename P::Acc (&acc)[R][COUTP / 16]) {
   using DV = typename P::DV;
+  constexpr int NT = COUTP / 16;
   const int off = ((kc * 4 + g) ^ sw) * 16;
   DV xs[R + 2];
 #pragma unroll
   for (int i = 0; i < R + 2; ++i) xs[i] = P::ld_lds(X + rb[i] + off);
   DV w[9];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) w[k] = ws.dwv(k, kc, g);
+  ws.dw_taps(kc, g, w);
+  // A fragments one tile ahead (two registers): with one register the compiler serialises
+  // `ds_read -> s_waitcnt -> MFMA x R` per tile and exposes the LDS latency NT times a chunk
+  DV a_cur = ws.afrag(0, kc, lane, g);
   DV d[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) d[r] = P::dw_row(xs[r], xs[r + 1], xs[r + 2], w);
 #pragma unroll
-  for (int n = 0; n < COUTP / 16; ++n) {
-    const DV a = ws.afrag(n, kc, lane, g);
+  for (int n = 0; n < NT; ++n) {
+    DV a_nxt = a_cur;
+    if (n + 1 < NT) a_nxt = ws.afrag(n + 1, kc, lane, g);
     if constexpr (FIRST) {
       const typename P::Acc bn = ws.bias_acc(n, g);
 #pragma unroll
-      for (int r = 0; r < R; ++r) acc[r][n] = P::mma_v(a, d[r], bn);
+      for (int r = 0; r < R; ++r) acc[r][n] = P::mma_v(a_cur, d[r], bn);
     } else {
 #pragma unroll
-      for (int r = 0; r < R; ++r) acc[r][n] = P::mma_v(a, d[r], acc[r][n]);
+      for (int r = 0; r < R; ++r) acc[r][n] = P::mma_v(a_cur, d[r], acc[r][n]);
     }
+    a_cur = a_nxt;
   }
 }
 
@@ -392,11 +413,19 @@ __device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int
   constexpr int NKC = CINP / P::KC;
   const int sw = swz<NQ>(t);
   int rb[R + 2];
+  if constexpr (P::WLDS) {
+    // f16 layers have no inactive passes: rows s0-1 .. s0+R are inside the strip for every
+    // wave (conv1 [0, R0-1], conv2 [0, R0-3], conv3 [0, R0-4]), so no clamp -- the rows are
+    // then immediate offsets of one base register
 #pragma unroll
-  for (int i = 0; i < R + 2; ++i) {
-    int sl = s0 - 1 + i;
-    sl = sl < 0 ? 0 : (sl >= nslots ? nslots - 1 : sl);
-    rb[i] = sl * slot_pitch<P>() + t * NQ * 16;
+    for (int i = 0; i < R + 2; ++i) rb[i] = (s0 - 1 + i) * slot_pitch<P>() + t * NQ * 16;
+  } else {
+#pragma unroll
+    for (int i = 0; i < R + 2; ++i) {
+      int sl = s0 - 1 + i;
+      sl = sl < 0 ? 0 : (sl >= nslots ? nslots - 1 : sl);
+      rb[i] = sl * slot_pitch<P>() + t * NQ * 16;
+    }
   }
   conv_chunk<P, CINP, COUTP, true, R>(X, rb, sw, 0, g, lane, ws, acc);
   for (int kc = 1; kc < NKC; ++kc) conv_chunk<P, CINP, COUTP, false, R>(X, rb, sw, kc, g, lane, ws, acc);
@@ -1871,7 +1900,7 @@ int strip_width(int precision) { return precision == 0 ? P16::FO : P64::FO; }
 
 #ifdef NRX_STAMPS
 extern "C" int nrx_debug_stamps(void* out, int n) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nrx_stamps), (size_t)n * 32 * 8, 0, hipMemcpyDeviceToHost);
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nrx_stamps), (size_t)n * 64 * 8, 0, hipMemcpyDeviceToHost);
 }
 #endif
 

@@ -24,7 +24,7 @@ for _ in range(300):
     eng.forward(dy, pe, dh, da, None, 2, "f16")
 torch.cuda.synchronize()
 n = 512
-buf = np.zeros((n, 32), np.uint64)
+buf = np.zeros((n, 64), np.uint64)
 lib.nrx_debug_stamps(buf.ctypes.data, n)
 st = buf[:, [0, 1, 2, 3, 6, 4, 5]].astype(np.int64)
 d = np.diff(st, axis=1)
