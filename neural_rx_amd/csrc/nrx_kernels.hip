@@ -427,8 +427,47 @@ __device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int
       rb[i] = sl * slot_pitch<P>() + t * NQ * 16;
     }
   }
-  conv_chunk<P, CINP, COUTP, true, R>(X, rb, sw, 0, g, lane, ws, acc);
-  for (int kc = 1; kc < NKC; ++kc) conv_chunk<P, CINP, COUTP, false, R>(X, rb, sw, kc, g, lane, ws, acc);
+  if constexpr (P::WLDS) {
+    // software-pipelined over the K chunks: chunk kc+1's activation rows and depthwise taps
+    // are read into the registers of chunk kc as soon as its depthwise is done (they are
+    // dead then), so their LDS latency hides behind chunk kc's MFMAs instead of stalling the
+    // start of chunk kc+1
+    using DV = typename P::DV;
+    constexpr int NT = COUTP / 16;
+    DV xs[R + 2], w[9];
+    auto load = [&](int kc) {
+      const int off = ((kc * 4 + g) ^ sw) * 16;
+#pragma unroll
+      for (int i = 0; i < R + 2; ++i) xs[i] = P::ld_lds(X + rb[i] + off);
+      ws.dw_taps(kc, g, w);
+    };
+    load(0);
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc) {
+      DV a_cur = ws.afrag(0, kc, lane, g);
+      DV d[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) d[r] = P::dw_row(xs[r], xs[r + 1], xs[r + 2], w);
+      if (kc + 1 < NKC) load(kc + 1);
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        DV a_nxt = a_cur;
+        if (n + 1 < NT) a_nxt = ws.afrag(n + 1, kc, lane, g);
+        if (kc == 0) {
+          const typename P::Acc bn = ws.bias_acc(n, g);
+#pragma unroll
+          for (int r = 0; r < R; ++r) acc[r][n] = P::mma_v(a_cur, d[r], bn);
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) acc[r][n] = P::mma_v(a_cur, d[r], acc[r][n]);
+        }
+        a_cur = a_nxt;
+      }
+    }
+  } else {
+    conv_chunk<P, CINP, COUTP, true, R>(X, rb, sw, 0, g, lane, ws, acc);
+    for (int kc = 1; kc < NKC; ++kc) conv_chunk<P, CINP, COUTP, false, R>(X, rb, sw, kc, g, lane, ws, acc);
+  }
 }
 
 // One pass of a layer for one wave: R output rows from position p0 (act: any row valid).
@@ -750,6 +789,16 @@ struct CFrag {
         b[kc] = typename P::DV{(double)v[kc][0], (double)v[kc][1], (double)v[kc][2], (double)v[kc][3]};
     }
   }
+  // f16 policy: ReLU on the packed f16 fragments (v_pk_max_f16, two values an instruction)
+  // instead of on the f32 accumulators; round(relu(x)) == relu(round(x)) since rounding is
+  // monotone and keeps zero, so the layer outputs are unchanged
+  static constexpr bool kPackedRelu = P::KC == 32;
+  __device__ void relu() {
+    if constexpr (kPackedRelu) {
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc) b[kc] = __builtin_elementwise_max(b[kc], typename P::DV{});
+    }
+  }
 };
 
 // Dense layer over NR rows at once: every A fragment and bias tile is loaded once and
@@ -927,10 +976,14 @@ struct EpiConv3 {
   __device__ __forceinline__ void head_rows(const CFrag<P, NTS> (&sb)[RB], const W1& w1, const W2& w2, int lane,
                                             int g, Real (&o)[RB][NO][4]) const {
     Real hdn[RB][kHID / 16][4];
-    dense_rows<P, NTS, kHID, RB>(sb, w1, lane, g, hdn, true);
-    CFrag<P, kHID / 16> hb[RB];
+    using HF = CFrag<P, kHID / 16>;
+    dense_rows<P, NTS, kHID, RB>(sb, w1, lane, g, hdn, !HF::kPackedRelu);
+    HF hb[RB];
 #pragma unroll
-    for (int r = 0; r < RB; ++r) hb[r] = CFrag<P, kHID / 16>(hdn[r]);
+    for (int r = 0; r < RB; ++r) {
+      hb[r] = HF(hdn[r]);
+      hb[r].relu();
+    }
     dense_rows<P, kHID / 16, NO * 16, RB>(hb, w2, lane, g, o, false);
   }
 
@@ -1001,14 +1054,20 @@ struct EpiConv3 {
       } else if constexpr (P::WLDS) {
         DLds<P, kDSP> w1{WB + 16 * 1024, reinterpret_cast<const float*>(WB + kWTailBias)};
         DLds<P, kAGG> w2{WB + 24 * 1024, reinterpret_cast<const float*>(WB + kWTailBias + kAGG * 4)};
-        dense_rows<P, NTS, kAGG, R>(sb, w1, lane, g, hdn, true);
+        dense_rows<P, NTS, kAGG, R>(sb, w1, lane, g, hdn, !CFrag<P, kAGG / 16>::kPackedRelu);
 #pragma unroll
-        for (int r = 0; r < R; ++r) hb[r] = CFrag<P, kAGG / 16>(hdn[r]);
+        for (int r = 0; r < R; ++r) {
+          hb[r] = CFrag<P, kAGG / 16>(hdn[r]);
+          hb[r].relu();
+        }
         dense_rows<P, kAGG / 16, kDSP, R>(hb, w2, lane, g, sp, false);
       } else {
-        dense_rows<P, NTS, kAGG, R>(sb, DGlb<P, kDSP>{prm->agg[0]}, lane, g, hdn, true);
+        dense_rows<P, NTS, kAGG, R>(sb, DGlb<P, kDSP>{prm->agg[0]}, lane, g, hdn, !CFrag<P, kAGG / 16>::kPackedRelu);
 #pragma unroll
-        for (int r = 0; r < R; ++r) hb[r] = CFrag<P, kAGG / 16>(hdn[r]);
+        for (int r = 0; r < R; ++r) {
+          hb[r] = CFrag<P, kAGG / 16>(hdn[r]);
+          hb[r].relu();
+        }
         dense_rows<P, kAGG / 16, kDSP, R>(hb, DGlb<P, kAGG>{prm->agg[1]}, lane, g, sp, false);
       }
 #pragma unroll
