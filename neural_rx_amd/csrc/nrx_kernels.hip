@@ -742,8 +742,17 @@ struct DLds {
   const char* base;
   const float* bias_p;
   static constexpr int NQ = CINP * 2 / 16;
+  // Fragment address = one register per K chunk + the tile row as an immediate offset.  A
+  // plain `base + lds_off(n, ..)` compiles to or + shift + add per fragment: LLVM turns the
+  // disjoint-bit sum into an OR that the DS addressing match cannot split, and WB lies
+  // beyond the 16-bit offset range.  The asm (not volatile, so equal (base, kc) calls are
+  // CSE'd) hides the per-lane part from that rewrite.
   __device__ typename P::DV afrag(int n, int kc, int lane, int g) const {
-    return *reinterpret_cast<const half8*>(base + lds_off<NQ>(n, lane & 15, kc * 4 + g));
+    typedef const __attribute__((address_space(3))) char lds_char;
+    typedef const __attribute__((address_space(3))) half8 lds_half8;
+    unsigned a = (unsigned)(size_t)(lds_char*)base + (unsigned)lds_off<NQ>(0, lane & 15, kc * 4 + g);
+    asm("" : "+v"(a));
+    return *reinterpret_cast<lds_half8*>((lds_char*)(size_t)a + n * (kTP * NQ * 16));
   }
   __device__ typename P::Acc bias_acc(int n, int g) const { return P::bias_acc(bias_p, n, g); }
 };
