@@ -511,7 +511,9 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
         // conditional settle left the skip-row loads pending and the first use in the
         // epilogue waited for vmcnt(0), i.e. for the whole DMA.
         __syncthreads();
+        stamp(30);
         epi.next_hook();
+        stamp(31);
       }
     }
     if (act) epi.template run<R>(acc, pf, p0, t, g, 0, R);
@@ -1528,6 +1530,7 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
   stamp(1);
   strip_block<P, kUPD_CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 0, 0, false, nb, nu, nfs);
   stamp(4);
+  if (nb >= 0) stamp(32);   // first item of a pair done
 }
 
 #ifndef NRX_PAIR
