@@ -716,6 +716,8 @@ constexpr int strip_lds_bytes() {
 }
 static_assert(P16::FO <= 8 * P16::R, "the conv3 of a strip must run in one round");
 
+// in-plane element offset of (f, t) in a [F][14][56] state plane (< 2^31 for F <= 3276)
+__device__ __forceinline__ int sre(int f, int t) { return (f * kT + t) * kDS; }
 __device__ __forceinline__ size_t srow(int b, int u, int f, int t, int U, int F) {
   return ((((size_t)b * U + u) * F + f) * kT + t) * kDS;
 }
@@ -896,8 +898,9 @@ struct EpiConv3 {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const bool ok = need && row_ok(p0 + r, t);
-      const size_t off = srow(b, u, ok ? f_start + p0 + r : 0, ok ? t : 0, a.U, a.F);
-      const S* src = (mode == 0 ? a.s_in : a.s_out) + off;
+      // uniform plane base + 32-bit in-plane offset (no per-row 64-bit index chain)
+      const S* src = (mode == 0 ? a.s_in : a.s_out) + srow(b, u, 0, 0, a.U, a.F) +
+                     sre(ok ? f_start + p0 + r : 0, ok ? t : 0);
 #pragma unroll
       for (int n = 0; n < NTS; ++n) {
         if constexpr (sizeof(S) == 2) {
@@ -1026,7 +1029,7 @@ struct EpiConv3 {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       ok[r] = row_ok(p0 + r, t) && !(NRX_ABLATE & 16);
-      off[r] = srow(b, u, ok[r] ? f_start + p0 + r : 0, ok[r] ? t : 0, U, F);
+      off[r] = srow(b, u, 0, 0, U, F) + (size_t)(unsigned)sre(ok[r] ? f_start + p0 + r : 0, ok[r] ? t : 0);
     }
     if constexpr (TAILM != TAIL_READOUT) {
 #pragma unroll
@@ -1472,19 +1475,23 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
   const bool has_a = U == 2;
   typedef __attribute__((address_space(3))) void lds_void;
   typedef const __attribute__((address_space(1))) void glb_void;
-  for (int k = wave; k < R0 * 4; k += 8) {
-    const int r = k >> 2, t = 4 * (k & 3) + tq;
-    const int f = f_start + r;
-    const int q = qp ^ swz<16>(t);
-    const S* src = reinterpret_cast<const S*>(g_zero16);
-    if (t < kT && f >= 0 && f < F) {
-      const int re = (f * kT + t) * kDS;
-      if (q < QS) {
-        if (has_a) src = ap + re + P::EPC * q;
-      } else if (q < 2 * QS) {
-        src = sp + re + P::EPC * (q - QS);
-      }
+  // instruction k = wave + 8 i covers slot r = (wave >> 2) + 2 i, symbols 4 (wave & 3) + tq:
+  // the lane's symbol and chunk (hence its source plane and column) are loop-invariant, only
+  // the slot advances, so the per-lane source is computed once and stepped by two grid rows
+  const int t = 4 * (wave & 3) + tq;
+  const int q = qp ^ swz<16>(t);
+  const S* lsrc = nullptr;   // this lane's chunk in grid row 0 (null: always zero)
+  if (t < kT) {
+    if (q < QS) {
+      if (has_a) lsrc = ap + t * kDS + P::EPC * q;
+    } else if (q < 2 * QS) {
+      lsrc = sp + t * kDS + P::EPC * (q - QS);
     }
+  }
+  for (int k = wave; k < R0 * 4; k += 8) {
+    const int f = f_start + (k >> 2);             // wave-uniform
+    const S* src = reinterpret_cast<const S*>(g_zero16);
+    if (f >= 0 && f < F && lsrc) src = lsrc + (size_t)f * (kT * kDS);
     __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(X + k * 1024), 16, 0, 0);
   }
 }
