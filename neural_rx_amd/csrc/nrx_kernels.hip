@@ -62,8 +62,16 @@ __device__ __forceinline__ void stamp(int k) {
     if (wg < 4096) g_nrx_stamps[wg][k] = __builtin_amdgcn_s_memtime();
   }
 }
+// per-wave stamp k + wave (lane 0 of every wave), k in {40, 48, 56}
+__device__ __forceinline__ void stamp_w(int k) {
+  if ((threadIdx.x & 63) == 0 && g_nrx_stamp_on) {
+    const int wg = blockIdx.x;
+    if (wg < 4096) g_nrx_stamps[wg][k + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime();
+  }
+}
 #else
 __device__ __forceinline__ void stamp(int) {}
+__device__ __forceinline__ void stamp_w(int) {}
 #endif
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -496,6 +504,7 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
     }
   }
   stamp(9 + 5 * in_off);
+  if (in_off == 0) stamp_w(40);
   if constexpr (E::kNoBarrier) {
     // the epilogue neither writes LDS nor reads anything staged after the math: each
     // wave runs it as soon as its own math is done (post_math is empty for these)
@@ -523,6 +532,7 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
     // round (wave w-1 reads up to slot p0 - in_off): written before the barrier
     constexpr int ER = E::kEarlyRow < R ? E::kEarlyRow : R;
     if (act) epi.template run<R>(acc, pf, p0, t, g, ER, R);
+    if (in_off == 0) stamp_w(48);
     __syncthreads();
     stamp(10 + 5 * in_off);
     if (first_round) post_math();      // all threads: this layer's weights are dead (P16)
@@ -530,6 +540,7 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
     stamp(11 + 5 * in_off);
     if (act) epi.template run<R>(acc, pf, p0, t, g, 0, ER);
     stamp(12 + 5 * in_off);
+    if (in_off == 0) stamp_w(56);
     __syncthreads();
   }
 }
@@ -588,33 +599,49 @@ struct EpiInPlace {
     using Real = typename P::Real;
     using S = typename P::S;
     constexpr int NQ = COUTP * (int)sizeof(S) / 16;
+    if constexpr (sizeof(S) == 2) {
+      // f16: lane (t, g) holds 4 channels of each tile (8 bytes of chunk 2n + (g >> 1)).
+      // The lane's per-tile addresses are formed once per pass (opaque to LLVM so that
+      // they stay registers); a row adds r * slot_pitch as the DS immediate offset.
+      typedef __attribute__((address_space(3))) half4 lds_half4;
+      constexpr int NT = COUTP / 16;
+      unsigned lo[NT];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (r < r_lo || r >= r_hi) continue;
-      const int p = p0 + r;
-      if (p >= pos_hi) continue;
-      const int f = f_start + p;
-      const bool z = f < 0 || f >= F;
-      const int slot = p - in_off - 1;
-      if constexpr (sizeof(S) == 2) {
-        // p0 (hence p, f, z, slot) is wave-uniform: the grid-edge test is a scalar branch,
-        // and the row's slot offset is added to per-tile lane offsets computed once
-        char* row = X + slot * slot_pitch<P>();
-        if (t < kT) {
+      for (int n = 0; n < NT; ++n) {
+        lo[n] = (unsigned)(size_t)(__attribute__((address_space(3))) char*)X +
+                (unsigned)((p0 - in_off - 1) * slot_pitch<P>() + lane_off(n, t, g));
+        asm("" : "+v"(lo[n]));
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r < r_lo || r >= r_hi) continue;
+        const int p = p0 + r;
+        if (p >= pos_hi) continue;
+        const int f = f_start + p;
+        const bool z = f < 0 || f >= F;   // wave-uniform: scalar branch
+        if (t < kT) {   // pad symbols t >= 14 stay zero from the start of the block
           if (!z) {
 #pragma unroll
-            for (int n = 0; n < COUTP / 16; ++n) {
+            for (int n = 0; n < NT; ++n) {
               half4 h = half4{(S)acc[r][n][0], (S)acc[r][n][1], (S)acc[r][n][2], (S)acc[r][n][3]};
               h = __builtin_elementwise_max(h, half4{0, 0, 0, 0});
-              *reinterpret_cast<half4*>(row + lane_off(n, t, g)) = h;
+              *(lds_half4*)(size_t)(lo[n] + r * slot_pitch<P>()) = h;
             }
           } else {
 #pragma unroll
-            for (int n = 0; n < COUTP / 16; ++n)
-              *reinterpret_cast<half4*>(row + lane_off(n, t, g)) = half4{0, 0, 0, 0};
+            for (int n = 0; n < NT; ++n) *(lds_half4*)(size_t)(lo[n] + r * slot_pitch<P>()) = half4{0, 0, 0, 0};
           }
         }
-      } else {
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r < r_lo || r >= r_hi) continue;
+        const int p = p0 + r;
+        if (p >= pos_hi) continue;
+        const int f = f_start + p;
+        const bool z = f < 0 || f >= F;
+        const int slot = p - in_off - 1;
 #pragma unroll
         for (int n = 0; n < COUTP / 16; ++n) {
 #pragma unroll

@@ -67,3 +67,11 @@ for L in range(3):
     seg = np.diff(det[:, L, :], axis=1)
     print(f"  (last item) conv{L + 1}: math {seg[:, 0].mean():7.0f}  bar1 {seg[:, 1].mean():7.0f}  "
           f"post {seg[:, 2].mean():7.0f}  epi {seg[:, 3].mean():7.0f}")
+# per-wave conv1 stamps (last item of the workgroup): 40+w math end, 48+w early rows stored
+# (before the layer barrier), 56+w rows 0,1 stored; relative to wave 0's conv1 math start (8)
+if (buf[:, 40:64] > 0).any():
+    base = buf[:, 8:9]
+    for k, name in ((40, "math end"), (48, "pre-barrier"), (56, "rows 0,1 stored")):
+        v = (buf[:, k:k + 8] - base).mean(axis=0)
+        print(f"  conv1 per wave {name:16s}", " ".join(f"{x:7.0f}" for x in v))
+    print(f"  conv1 barrier release (stamp 10) {float((buf[:, 10] - buf[:, 8]).mean()):7.0f}")
