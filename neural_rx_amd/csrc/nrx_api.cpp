@@ -224,17 +224,24 @@ int build_model(const nrx_desc* d, const float* const* w, int kc, DeviceModel<WT
     k += 2;
     return r;
   };
+  // f16: conv2 / conv3 read the strip image the previous layer's in-place epilogue wrote
+  // straight from its accumulators (lane (t, g) stores tiles 2kc, 2kc+1 as one 16-byte
+  // chunk 4kc + g), i.e. their input channels sit in the K-permuted order of the dense
+  // layers: channel c at packed position kperm^-1(c)
+  std::vector<int> hpos(kHID);
+  for (int p = 0; p < kHID; ++p) hpos[Packer<WT, BT>::kperm_channel(p, kc == 32 ? 32 : 0)] = p;
+  const std::vector<int>* hp = kc == 32 ? &hpos : nullptr;
   for (int m = 0; m < num_init(d); ++m) {
     init[m][0] = sep(icin, kHID, icinp, kHID, &ipos);
-    init[m][1] = sep(kHID, kHID, kHID, kHID);
-    init[m][2] = sep(kHID, kDS, kHID, kDSP);
+    init[m][1] = sep(kHID, kHID, kHID, kHID, hp);
+    init[m][2] = sep(kHID, kDS, kHID, kDSP, hp);
   }
   for (int i = 0; i < d->num_it; ++i) {
     agg[i][0] = den(kDS, kAGG, kDSP, kAGG);
     agg[i][1] = den(kAGG, kDS, kAGG, kDSP);
     upd[i][0] = sep(2 * kDS + 2, kHID, kUPD_CINP, kHID);
-    upd[i][1] = sep(kHID, kHID, kHID, kHID);
-    upd[i][2] = sep(kHID, kDS, kHID, kDSP);
+    upd[i][1] = sep(kHID, kHID, kHID, kHID, hp);
+    upd[i][2] = sep(kHID, kDS, kHID, kDSP, hp);
   }
   for (int h = 0; h < num_heads(d); ++h) {
     const int nb = d->var_mcs_masking ? bits_max(d) : d->bits[h];

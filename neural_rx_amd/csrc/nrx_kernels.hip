@@ -588,11 +588,6 @@ struct EpiInPlace {
   __device__ void pre() const {}
   template <int R>
   __device__ void prefetch(NoPref&, int, int, int) const {}
-  // byte offset of lane (t, g)'s 4 channels of tile n inside a slot (f16 layout)
-  __device__ static int lane_off(int n, int t, int g) {
-    constexpr int NQ = COUTP * 2 / 16;
-    return xoff<P, NQ>(0, t, 2 * n + (g >> 1)) + (g & 1) * 8;
-  }
   template <int R>
   __device__ void run(const typename P::Acc (&acc)[R][COUTP / 16], const NoPref&, int p0, int t,
                       int g, int r_lo, int r_hi) const {
@@ -600,17 +595,20 @@ struct EpiInPlace {
     using S = typename P::S;
     constexpr int NQ = COUTP * (int)sizeof(S) / 16;
     if constexpr (sizeof(S) == 2) {
-      // f16: lane (t, g) holds 4 channels of each tile (8 bytes of chunk 2n + (g >> 1)).
-      // The lane's per-tile addresses are formed once per pass (opaque to LLVM so that
-      // they stay registers); a row adds r * slot_pitch as the DS immediate offset.
-      typedef __attribute__((address_space(3))) half4 lds_half4;
-      constexpr int NT = COUTP / 16;
-      unsigned lo[NT];
+      // f16: the image of an in-place layer's output is in the K-permuted channel order of
+      // the consumer (nrx_api.cpp build_model, hpos): lane (t, g)'s 4 channels of tiles
+      // 2kc and 2kc+1 are chunk 4kc + g, so each tile pair is one 16-byte store of the
+      // lane's own values.  The lane's chunk addresses are formed once per pass (opaque
+      // to LLVM so that they stay registers); a row adds r * slot_pitch as the DS
+      // immediate offset.
+      typedef __attribute__((address_space(3))) half8 lds_half8;
+      constexpr int NKC = COUTP / 32;
+      unsigned lo[NKC];
 #pragma unroll
-      for (int n = 0; n < NT; ++n) {
-        lo[n] = (unsigned)(size_t)(__attribute__((address_space(3))) char*)X +
-                (unsigned)((p0 - in_off - 1) * slot_pitch<P>() + lane_off(n, t, g));
-        asm("" : "+v"(lo[n]));
+      for (int kc = 0; kc < NKC; ++kc) {
+        lo[kc] = (unsigned)(size_t)(__attribute__((address_space(3))) char*)X +
+                 (unsigned)((p0 - in_off - 1) * slot_pitch<P>() + (t * NQ + ((4 * kc + g) ^ swz<NQ>(t))) * 16);
+        asm("" : "+v"(lo[kc]));
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -622,14 +620,16 @@ struct EpiInPlace {
         if (t < kT) {   // pad symbols t >= 14 stay zero from the start of the block
           if (!z) {
 #pragma unroll
-            for (int n = 0; n < NT; ++n) {
-              half4 h = half4{(S)acc[r][n][0], (S)acc[r][n][1], (S)acc[r][n][2], (S)acc[r][n][3]};
-              h = __builtin_elementwise_max(h, half4{0, 0, 0, 0});
-              *(lds_half4*)(size_t)(lo[n] + r * slot_pitch<P>()) = h;
+            for (int kc = 0; kc < NKC; ++kc) {
+              const auto& a0 = acc[r][2 * kc];
+              const auto& a1 = acc[r][2 * kc + 1];
+              half8 h = half8{(S)a0[0], (S)a0[1], (S)a0[2], (S)a0[3], (S)a1[0], (S)a1[1], (S)a1[2], (S)a1[3]};
+              h = __builtin_elementwise_max(h, half8{});
+              *(lds_half8*)(size_t)(lo[kc] + r * slot_pitch<P>()) = h;
             }
           } else {
 #pragma unroll
-            for (int n = 0; n < NT; ++n) *(lds_half4*)(size_t)(lo[n] + r * slot_pitch<P>()) = half4{0, 0, 0, 0};
+            for (int kc = 0; kc < NKC; ++kc) *(lds_half8*)(size_t)(lo[kc] + r * slot_pitch<P>()) = half8{};
           }
         }
       }
