@@ -263,6 +263,20 @@ constexpr int kWDw = 9 * kHID * 2;             // 2304 B
 constexpr int kWBias = kWPw + kWDw;            // conv bias [COUTP] f32
 constexpr int kWTailBias = kWBias + kHID * 4;  // aggregation-MLP biases (2 x 64 f32)
 constexpr int kWBytes = kWTailBias + 2 * kAGG * 4;
+// The paired readout tail gives WB the rest of the 160 KB LDS (P16: 160 KB - 30 x 4 KB) and
+// stages the heads there, so that the strip image X is free for the next item's z DMA
+// during the readout epilogue.  W1^T images in full; W2^T images truncated to their real
+// rows (bits, 2A): the lanes of the padding rows read whatever follows, which only reaches
+// output channels that are never stored.  One LLR head only.
+constexpr int kWAlloc = 160 * 1024 - 30 * kTP * kHID * 2;
+static_assert(kWBytes <= kWAlloc, "layer weight image exceeds the LDS left by the strip image");
+constexpr int kHW1C = 16 * 1024;                 // ChEst W1^T (LLR W1^T at 0)
+constexpr int kHB1 = 32 * 1024;                  // b1: LLR [128] f32, ChEst [128] f32
+constexpr int kHB2 = kHB1 + 2 * kHID * 4;        // b2: LLR [16] f32, ChEst [<= 32] f32
+constexpr int kHW2 = kHB2 + (16 + 32) * 4;       // LLR W2^T rows [bits], then ChEst rows [2A]
+__host__ __device__ constexpr bool heads_fit_wb(int bits_max, int chp) {
+  return kHW2 + 256 * (bits_max + chp) <= kWAlloc;   // + the padding-row reads of ChEst
+}
 
 template <class P, int CINP, int COUTP>
 struct WLds {
@@ -361,11 +375,11 @@ struct DenseStage {
     }
     bias = threadIdx.x < COUTP ? w.b[threadIdx.x] : 0.f;
   }
-  __device__ void store(char* dst, float* bias_dst) const {
+  __device__ void store(char* dst, float* bias_dst, int rows = COUTP) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int idx = threadIdx.x + i * 512;
-      if (idx < NW) {
+      if (idx < NW && idx / NQ < rows) {
         const int co = idx / NQ, q = idx % NQ;
         *reinterpret_cast<intx4*>(dst + lds_off<NQ>(co >> 4, co & 15, q)) = v[i];
       }
@@ -532,11 +546,21 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
     // round (wave w-1 reads up to slot p0 - in_off): written before the barrier
     constexpr int ER = E::kEarlyRow < R ? E::kEarlyRow : R;
     if (act) epi.template run<R>(acc, pf, p0, t, g, ER, R);
+    if constexpr (E::kNextHookRO) epi.template settle<R>(pf);   // before any next-item DMA
     if (in_off == 0) stamp_w(48);
     __syncthreads();
     stamp(10 + 5 * in_off);
     if (first_round) post_math();      // all threads: this layer's weights are dead (P16)
     epi.pre();                       // all threads (e.g. stage tail weights into X)
+    if constexpr (E::kNextHookRO) {
+      // paired readout items: the heads are in WB and every wave is past its conv3 reads,
+      // so the next item's z image is DMA'd into X while this epilogue runs
+      if (epi.nb >= 0) {
+        stamp(30);
+        epi.next_hook();
+        stamp(31);
+      }
+    }
     stamp(11 + 5 * in_off);
     if (act) epi.template run<R>(acc, pf, p0, t, g, 0, ER);
     stamp(12 + 5 * in_off);
@@ -581,6 +605,7 @@ struct EpiInPlace {
   using PrefT = NoPref;
   static constexpr bool kNoBarrier = false;
   static constexpr bool kNextHook = false;
+  static constexpr bool kNextHookRO = false;
   static constexpr int kEarlyRow = 2;
   char* X;
   int in_off, pos_hi, f_start, F;
@@ -717,7 +742,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 //
 // State / aggregate buffers are compact: [B][U][F][14][56] (no padding in HBM).
 
-enum Tail { TAIL_NONE = -1, TAIL_AGG = 0, TAIL_READOUT = 1 };
+// TAIL_READOUT_WB: readout tail with the heads staged into WB, two items per workgroup
+enum Tail { TAIL_NONE = -1, TAIL_AGG = 0, TAIL_READOUT = 1, TAIL_READOUT_WB = 2 };
+constexpr bool readout_tail(int t) { return t == TAIL_READOUT || t == TAIL_READOUT_WB; }
 
 template <class P>
 struct BlockParams {
@@ -738,9 +765,10 @@ struct BlockParams {
 template <class P>
 constexpr int strip_slots() { return P::FO + 2 * kHalo; }
 template <class P>
-constexpr int strip_lds_bytes() {
-  return strip_slots<P>() * slot_pitch<P>() + (P::WLDS ? kWBytes : 0);
+constexpr int strip_lds_bytes(bool heads_wb = false) {
+  return strip_slots<P>() * slot_pitch<P>() + (P::WLDS ? (heads_wb ? kWAlloc : kWBytes) : 0);
 }
+static_assert(strip_lds_bytes<P16>(true) == 160 * 1024, "P16 strip image + WB = LDS");
 static_assert(P16::FO <= 8 * P16::R, "the conv3 of a strip must run in one round");
 
 // in-plane element offset of (f, t) in a [F][14][56] state plane (< 2^31 for F <= 3276)
@@ -891,8 +919,10 @@ struct EpiConv3 {
     std::conditional_t<sizeof(S) == 2, half4, Real[4]> prev[R][NTS];
   };
   // no LDS writes; the readout tail reads head weights staged into X after the math
-  static constexpr bool kNoBarrier = TAILM != TAIL_READOUT;
+  static constexpr bool kNoBarrier = !readout_tail(TAILM);
   static constexpr bool kNextHook = TAILM == TAIL_AGG && P::WLDS;
+  // paired readout items: the next z DMA is issued once the head weights are in WB
+  static constexpr bool kNextHookRO = TAILM == TAIL_READOUT_WB && P::WLDS;
   static constexpr int kEarlyRow = 8;      // readout: every row after the barrier
   const BlockParams<P>* prm;
   char* X;
@@ -948,7 +978,9 @@ struct EpiConv3 {
 
   __device__ void pre() const {
     if constexpr (P::WLDS) {
-      if constexpr (TAILM == TAIL_READOUT) {
+      if constexpr (TAILM == TAIL_READOUT_WB) {
+        __syncthreads();   // heads staged into WB by strip_block (one LLR head)
+      } else if constexpr (TAILM == TAIL_READOUT) {
         // LLR head 0 and the ChEst head were prefetched during the conv3 math and stored
         // into X by strip_block; stage any further heads (Var-IO) now
         const auto& a = prm->a;
@@ -1013,6 +1045,22 @@ struct EpiConv3 {
     }
   }
 
+  // LDS images of readout head hh (hh == H: ChEst): X layout (head_w1 ..) or, paired, WB
+  __device__ void head_lds(int hh, bool ch, const char*& w1, const float*& b1, const char*& w2,
+                           const float*& b2) const {
+    if constexpr (TAILM == TAIL_READOUT_WB) {
+      w1 = WB + (ch ? kHW1C : 0);
+      b1 = reinterpret_cast<const float*>(WB + kHB1 + (ch ? kHID * 4 : 0));
+      b2 = reinterpret_cast<const float*>(WB + kHB2 + (ch ? 16 * 4 : 0));
+      w2 = WB + kHW2 + (ch ? prm->a.bits_max * 256 : 0);
+    } else {
+      w1 = X + head_w1(hh);
+      b1 = reinterpret_cast<const float*>(X + head_b1(hh));
+      w2 = X + head_w2(hh);
+      b2 = reinterpret_cast<const float*>(X + head_b2(hh));
+    }
+  }
+
   template <int NO, int RB, class W1, class W2>
   __device__ __forceinline__ void head_rows(const CFrag<P, NTS> (&sb)[RB], const W1& w1, const W2& w2, int lane,
                                             int g, Real (&o)[RB][NO][4]) const {
@@ -1058,7 +1106,7 @@ struct EpiConv3 {
       ok[r] = row_ok(p0 + r, t) && !(NRX_ABLATE & 16);
       off[r] = srow(b, u, 0, 0, U, F) + (size_t)(unsigned)sre(ok[r] ? f_start + p0 + r : 0, ok[r] ? t : 0);
     }
-    if constexpr (TAILM != TAIL_READOUT) {
+    if constexpr (!readout_tail(TAILM)) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         S* dst = a.s_out + off[r];
@@ -1146,9 +1194,10 @@ struct EpiConv3 {
           if (!ch) {
             Real o[RB][1][4];
             if constexpr (P::WLDS) {
-              head_rows<1, RB>(sbr, DLds<P, kDSP>{X + head_w1(hh), reinterpret_cast<const float*>(X + head_b1(hh))},
-                               DLds<P, kHID>{X + head_w2(hh), reinterpret_cast<const float*>(X + head_b2(hh))},
-                               lane, g, o);
+              const char *w1, *w2;
+              const float *b1, *b2;
+              head_lds(hh, false, w1, b1, w2, b2);
+              head_rows<1, RB>(sbr, DLds<P, kDSP>{w1, b1}, DLds<P, kHID>{w2, b2}, lane, g, o);
             } else {
               head_rows<1, RB>(sbr, DGlb<P, kDSP>{prm->llr[hh][0]}, DGlb<P, kHID>{prm->llr[hh][1]}, lane, g, o);
             }
@@ -1178,10 +1227,10 @@ struct EpiConv3 {
           } else {
             Real o[RB][CHP / 16][4];
             if constexpr (P::WLDS) {
-              head_rows<CHP / 16, RB>(sbr,
-                                      DLds<P, kDSP>{X + head_w1(hh), reinterpret_cast<const float*>(X + head_b1(hh))},
-                                      DLds<P, kHID>{X + head_w2(hh), reinterpret_cast<const float*>(X + head_b2(hh))},
-                                      lane, g, o);
+              const char *w1, *w2;
+              const float *b1, *b2;
+              head_lds(hh, true, w1, b1, w2, b2);
+              head_rows<CHP / 16, RB>(sbr, DLds<P, kDSP>{w1, b1}, DLds<P, kHID>{w2, b2}, lane, g, o);
             } else {
               head_rows<CHP / 16, RB>(sbr, DGlb<P, kDSP>{prm->chest[0]}, DGlb<P, kHID>{prm->chest[1]}, lane, g, o);
             }
@@ -1271,13 +1320,21 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
         c2.load(prm.chest[1]);
       }
     };
-    if constexpr (P::WLDS && TAILM == TAIL_READOUT && kPrefetchW) ld();
+    if constexpr (P::WLDS && readout_tail(TAILM) && kPrefetchW) ld();
     run_layer<P, kHID, kDSP>(X, WB, prm.w[2], 2, kHalo, R0 - kHalo, [&](auto ws) {
       return EpiConv3<P, decltype(ws), CHP, TAILM>{&prm, X, WB, ws, b, u, f_start, R0 - kHalo, mode, wm, first,
                                                    (typename P::Real)prm.a.active[(size_t)b * prm.a.U + u],
                                                    nb, nu, nfs};
     }, [&]() {
-      if constexpr (P::WLDS && TAILM == TAIL_READOUT) {
+      if constexpr (P::WLDS && TAILM == TAIL_READOUT_WB) {
+        // conv3's weights are dead (every wave is past its math): heads into WB
+        if constexpr (!kPrefetchW) ld();
+        const int nb2 = prm.a.bits_max;
+        l1.store(WB, reinterpret_cast<float*>(WB + kHB1));
+        c1.store(WB + kHW1C, reinterpret_cast<float*>(WB + kHB1 + kHID * 4));
+        l2.store(WB + kHW2, reinterpret_cast<float*>(WB + kHB2), nb2);
+        c2.store(WB + kHW2 + nb2 * 256, reinterpret_cast<float*>(WB + kHB2 + 16 * 4), 2 * prm.a.A);
+      } else if constexpr (P::WLDS && TAILM == TAIL_READOUT) {
         if constexpr (!kPrefetchW) ld();
         const int H = prm.a.H;
         l1.store(X + head_w1(0), reinterpret_cast<float*>(X + head_b1(0)));
@@ -1525,7 +1582,7 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
 
 template <class P, class WS, int CHP, int TAILM>
 __device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook() const {
-  if constexpr (kNextHook) zload_dma_u2<P>(*prm, X, nb, nu, nfs);
+  if constexpr (kNextHook || kNextHookRO) zload_dma_u2<P>(*prm, X, nb, nu, nfs);
 }
 
 // Rest of an update item whose z image is being filled by LDS-DMA (issued by the caller, or
@@ -1570,11 +1627,14 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
 #ifndef NRX_PAIR
 #define NRX_PAIR 1
 #endif
+#ifndef NRX_PAIR_RO
+#define NRX_PAIR_RO 1
+#endif
 
 // Two update items (aggregation tail) per workgroup: item 1's z image is DMA'd into the
 // strip image during item 0's epilogue (EpiConv3::next_hook), so its load overlaps that
 // epilogue instead of stalling a chip-wide load phase of its own.
-template <class P, int CHP>
+template <class P, int CHP, int TAILM>
 __device__ __forceinline__ void update_pair(const BlockParams<P>& prm, char* smem, int b0, int u0, int s0, int b1,
                                             int u1, int s1) {
   constexpr int R0 = strip_slots<P>();
@@ -1582,8 +1642,8 @@ __device__ __forceinline__ void update_pair(const BlockParams<P>& prm, char* sme
   char* WB = smem + R0 * slot_pitch<P>();
   const int fs0 = s0 * P::FO - kHalo, fs1 = s1 * P::FO - kHalo;
   zload_dma_u2<P>(prm, X, b0, u0, fs0);
-  dma_item_run<P, CHP, TAIL_AGG>(prm, X, WB, b0, u0, fs0, b1, u1, fs1);
-  dma_item_run<P, CHP, TAIL_AGG>(prm, X, WB, b1, u1, fs1, -1, 0, 0);
+  dma_item_run<P, CHP, TAILM>(prm, X, WB, b0, u0, fs0, b1, u1, fs1);
+  dma_item_run<P, CHP, TAILM>(prm, X, WB, b1, u1, fs1, -1, 0, 0);
 }
 
 // UpdateState of user u on the strip (z = [a, s, pe]).
@@ -1823,11 +1883,11 @@ __global__ __launch_bounds__(512) void k_update(BlockParams<P> prm) {
   int b, u, strip;
   work_item(blockIdx.x, prm.a.B, prm.a.U, prm.strips, prm.order_rev, b, u, strip);
   stamp(0);
-  if constexpr (TAILM == TAIL_AGG && P::WLDS && NRX_PAIR != 0 && NRX_ZDMA != 0) {
+  if constexpr ((TAILM == TAIL_AGG || TAILM == TAIL_READOUT_WB) && P::WLDS && NRX_PAIR != 0 && NRX_ZDMA != 0) {
     if (prm.pair) {
       int b1, u1, s1;
       work_item(blockIdx.x + gridDim.x, prm.a.B, prm.a.U, prm.strips, prm.order_rev, b1, u1, s1);
-      update_pair<P, CHP>(prm, smem, b, u, strip, b1, u1, s1);
+      update_pair<P, CHP, TAILM>(prm, smem, b, u, strip, b1, u1, s1);
       stamp(5);
       return;
     }
@@ -1855,8 +1915,8 @@ struct Launch {
 
   static hipError_t setup() {
     hipError_t e = hipSuccess;
-    auto set = [&](const void* f) {
-      hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, strip_lds_bytes<P>());
+    auto set = [&](const void* f, bool heads_wb = false) {
+      hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, strip_lds_bytes<P>(heads_wb));
       if (r != hipSuccess) e = r;
     };
 #define NRX_SET_INIT(A2P)                                     \
@@ -1868,6 +1928,10 @@ struct Launch {
     set((const void*)k_update<P, 16, TAIL_READOUT>);
     set((const void*)k_update<P, 32, TAIL_AGG>);
     set((const void*)k_update<P, 32, TAIL_READOUT>);
+    if constexpr (P::WLDS) {
+      set((const void*)k_update<P, 16, TAIL_READOUT_WB>, true);
+      set((const void*)k_update<P, 32, TAIL_READOUT_WB>, true);
+    }
     return e;
   }
 
@@ -1957,8 +2021,27 @@ struct Launch {
       }
 #endif
       if (last) {
-        if (ch32) k_update<P, 32, TAIL_READOUT><<<grid, 512, L, st>>>(bp);
-        else k_update<P, 16, TAIL_READOUT><<<grid, 512, L, st>>>(bp);
+        // paired readout items (heads staged into WB) under the same conditions as the
+        // aggregation pairing below, for one LLR head that fits WB
+        bool pair_ro = false;
+        if constexpr (P::WLDS) {
+          const int items = (int)grid.x;
+          pair_ro = NRX_PAIR != 0 && NRX_ZDMA != 0 && NRX_PAIR_RO != 0 && args.U <= 2 && bp.inline_combine &&
+                    items % 16 == 0 && items >= 2 * cu_count() && args.H == 1 &&
+                    heads_fit_wb(args.bits_max, ch32 ? 32 : 16);
+          if (pair_ro) {
+            constexpr int L_wb = strip_lds_bytes<P>(true);
+            bp.pair = 1;
+            const dim3 g2(items / 2);
+            if (ch32) k_update<P, 32, TAIL_READOUT_WB><<<g2, 512, L_wb, st>>>(bp);
+            else k_update<P, 16, TAIL_READOUT_WB><<<g2, 512, L_wb, st>>>(bp);
+            bp.pair = 0;
+          }
+        }
+        if (!pair_ro) {
+          if (ch32) k_update<P, 32, TAIL_READOUT><<<grid, 512, L, st>>>(bp);
+          else k_update<P, 16, TAIL_READOUT><<<grid, 512, L, st>>>(bp);
+        }
       } else {
         // two items per workgroup when there are at least two per CU (CU count of the
         // device, one workgroup per CU by LDS) and the halves keep the XCD grouping of
