@@ -1373,10 +1373,30 @@ __device__ __forceinline__ double sq4(double acc, floatx4 v) {
   return __builtin_fma((double)v[3], (double)v[3], acc);
 }
 
-__device__ __forceinline__ double slot_norm(const float* y, int nq, double* red) {
+// The first kNormPre float4s of each thread are loaded up front (slot_norm_issue, from
+// clamped addresses, unconditionally) so that their latency overlaps the z-row loads; the
+// accumulation order is the plain strided loop's.
+constexpr int kNormPre = 4;
+struct NormPre {
+  floatx4 v[kNormPre];
+};
+__device__ __forceinline__ NormPre slot_norm_issue(const float* y, int nq) {
+  const floatx4* yq = reinterpret_cast<const floatx4*>(y);
+  NormPre p;
+#pragma unroll
+  for (int k = 0; k < kNormPre; ++k) {
+    const int i = threadIdx.x + 512 * k;
+    p.v[k] = yq[i < nq ? i : nq - 1];
+  }
+  return p;
+}
+__device__ __forceinline__ double slot_norm(const NormPre& pre, const float* y, int nq, double* red) {
   const floatx4* yq = reinterpret_cast<const floatx4*>(y);
   double acc = 0.0;
-  for (int i = threadIdx.x; i < nq; i += 512) {
+#pragma unroll
+  for (int k = 0; k < kNormPre; ++k)
+    if (threadIdx.x + 512 * k < nq) acc = sq4(acc, pre.v[k]);
+  for (int i = threadIdx.x + 512 * kNormPre; i < nq; i += 512) {
     const floatx4 v = yq[i];
     acc = sq4(acc, v);
   }
@@ -1442,6 +1462,11 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
   }
   SepStage<CINP, kHID> w1;
   if constexpr (P::WLDS) w1.load(prm.w[0]);
+  // small grids: the slot norm's y loads go out first, beside the z-row loads below
+  const float* yslot = a.y + (size_t)b * F * kT * A2;
+  const int nqs = F * kT * A2 / 4;
+  NormPre npre;
+  if (!prm.norm_pre) npre = slot_norm_issue(yslot, nqs);
   static_assert(R0 * kTP <= 512, "one z row per thread");
   {
     const int lf = threadIdx.x / kTP, tt = threadIdx.x % kTP;
@@ -1499,9 +1524,11 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
     }
     float2 pv = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + (ok ? f : 0)) * kT + (ok ? tt : 0)) * 2);
     if (!ok) pv = float2{0.f, 0.f};
+    stamp(33);
     // large grids: the per-slot k_norm pass already reduced y (every workgroup of the slot
     // re-reading the whole grid costs O(strips x grid) there); small grids: fused here
-    const Real ns = prm.norm_pre ? (Real)a.norm[b] : (Real)slot_norm(a.y + (size_t)b * F * kT * A2, F * kT * A2 / 4, red);
+    const Real ns = prm.norm_pre ? (Real)a.norm[b] : (Real)slot_norm(npre, yslot, nqs, red);
+    stamp(36);
     if (lf < R0) {
 #pragma unroll
       for (int q = 0; q < NQZ; ++q) {
@@ -1520,7 +1547,9 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
       }
     }
   }
+  stamp(37);
   if constexpr (P::WLDS) w1.store(WB);
+  stamp(39);
   __syncthreads();
   stamp(1);
   strip_block<P, CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 1, wm, first);

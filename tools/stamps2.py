@@ -48,7 +48,8 @@ buf = buf[used]
 st0 = buf[:, 0:1]
 rel = buf - st0
 print("launch", os.environ.get("NRX_STAMP_LAUNCH", "0"), f"workgroups {used.sum()}")
-order = [("pair: next z DMA issue", 30), ("pair: DMA issued", 31), ("pair: item 1 done", 32),
+order = [("init: loads issued", 33), ("init: slot norm", 36), ("init: z stored", 37), ("init: w1 stored", 39),
+         ("pair: next z DMA issue", 30), ("pair: DMA issued", 31), ("pair: item 1 done", 32),
          ("dma issue start", 24), ("dma issued", 25), ("conv1 start", 1), ("conv1 end", 2), ("conv2 end", 3),
          ("epilogue start", 6), ("item 1 end", 4), ("item 2 start", 26), ("item 2 data in", 27),
          ("item 2 block", 28), ("item 2 conv1 end", 34), ("item 2 conv2 end", 35),
