@@ -40,7 +40,8 @@ def main(fdir, wdir, key, num_it=2):
         out[short] = {"fetch_bytes_corrected": 2 * fe[k] * 1024, "write_bytes": wr.get(k, 0.0) * 1024}
         out[short]["bytes"] = out[short]["fetch_bytes_corrected"] + out[short]["write_bytes"]
     upd_mid = [v["bytes"] for k, v in out.items() if k.startswith("nrx::k_update") and k.endswith(", 0>")]
-    upd_last = [v["bytes"] for k, v in out.items() if k.startswith("nrx::k_update") and k.endswith(", 1>")]
+    # last iteration: readout tail (", 1>") or its paired heads-in-WB form (", 2>")
+    upd_last = [v["bytes"] for k, v in out.items() if k.startswith("nrx::k_update") and k.endswith((", 1>", ", 2>"))]
     rec = {"kernels": out, "unit": "bytes per launch",
            "note": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), rocprofv3 separate --pmc passes"}
     if upd_mid and upd_last:
