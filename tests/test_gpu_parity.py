@@ -149,13 +149,18 @@ def test_receiver_layouts_consistent():
 # item per workgroup): a slot's outputs must not depend on the batch it runs in or on which
 # workgroup ran it.  Cases: the bench shape; U = 1 (no other user: zero aggregate chunks);
 # a random active mask (act = 0 users, p = 1 / (#active - 1)); B = 136 (not a multiple of 8:
-# work_item's plain-order tail); F = 60 (a partial last strip, 3 strips).
+# work_item's plain-order tail); F = 60 (a partial last strip, 3 strips).  The last update
+# pairs too when its heads fit beside the strip image (TAIL_READOUT_WB: one LLR head, W2
+# rows truncated to the real bits / ChEst outputs): the 64-QAM masking model (6 bits, 8
+# iterations) covers a second truncation; Var-IO (two heads) keeps the unpaired readout.
 PAIRED_CASES = {
     "bench_b128_u2": dict(batch=128, users=2, prbs=4),
     "u1_b512": dict(batch=512, users=1, prbs=4),
     "random_active_b128": dict(batch=128, users=2, prbs=4, active="random"),
     "b136_tail": dict(batch=136, users=2, prbs=4),
     "f60_partial_strip": dict(batch=128, users=2, prbs=5),
+    "masking_64qam_b128": dict(config="nrx_large_var_mcs_64qam_masking", batch=128, users=2, prbs=4, snr_db=22),
+    "var_io_b128": dict(config="nrx_rt_var_mcs", batch=128, users=2, prbs=4),
 }
 
 
@@ -166,13 +171,17 @@ def test_batch_composition_invariance_paired_items(name):
     rng = np.random.default_rng(5)
     if kw.get("active") == "random":
         kw["active"] = (rng.random((kw["batch"], kw["users"])) < 0.6).astype(np.float32)
-    case = make_case("nrx_rt", snr_db=12, seed=11, **kw)
+    kw.setdefault("snr_db", 12)
+    case = make_case(kw.pop("config", "nrx_rt"), seed=11, **kw)
     eng = engine_for(case)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda()
-    llr, h = eng.forward(t(case.y), t(case.pe), t(case.h_hat), t(case.active), None, None, "f16")
+    multi = case.spec.num_mcs > 1
+    llr, h = eng.forward(t(case.y), t(case.pe), t(case.h_hat), t(case.active),
+                         t(case.mcs_mask) if multi else None, None, "f16")
     B = kw["batch"]
     sel = [0, 5, 77, B - 1]
-    llr4, h4 = eng.forward(t(case.y[sel]), t(case.pe), t(case.h_hat[sel]), t(case.active[sel]), None, None, "f16")
+    llr4, h4 = eng.forward(t(case.y[sel]), t(case.pe), t(case.h_hat[sel]), t(case.active[sel]),
+                           t(case.mcs_mask[sel]) if multi else None, None, "f16")
     torch.cuda.synchronize()
     assert np.array_equal(llr.cpu().numpy()[:, sel], llr4.cpu().numpy())
     assert np.array_equal(h.cpu().numpy()[sel], h4.cpu().numpy())
