@@ -161,6 +161,8 @@ PAIRED_CASES = {
     "f60_partial_strip": dict(batch=128, users=2, prbs=5),
     "masking_64qam_b128": dict(config="nrx_large_var_mcs_64qam_masking", batch=128, users=2, prbs=4, snr_db=22),
     "var_io_b128": dict(config="nrx_rt_var_mcs", batch=128, users=2, prbs=4),
+    # U = 8 > kInlineUsers: k_combine forms a_u in place (register z-load, unpaired)
+    "u8_combined_b16": dict(config="nrx_large_64qam", batch=16, users=8, prbs=8, snr_db=25),
 }
 
 
@@ -179,7 +181,7 @@ def test_batch_composition_invariance_paired_items(name):
     llr, h = eng.forward(t(case.y), t(case.pe), t(case.h_hat), t(case.active),
                          t(case.mcs_mask) if multi else None, None, "f16")
     B = kw["batch"]
-    sel = [0, 5, 77, B - 1]
+    sel = sorted({0, 5 % B, 77 % B, B - 1})
     llr4, h4 = eng.forward(t(case.y[sel]), t(case.pe), t(case.h_hat[sel]), t(case.active[sel]),
                            t(case.mcs_mask[sel]) if multi else None, None, "f16")
     torch.cuda.synchronize()
