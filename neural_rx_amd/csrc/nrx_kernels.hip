@@ -104,7 +104,11 @@ __device__ __forceinline__ half2 h2(half8 v, int k) {
   return half2{v[2 * k], v[2 * k + 1]};
 }
 
-struct P16 {
+// FO_: output subcarriers per strip.  P16 (24) is the throughput shape; P16S (8) is taken
+// for grids with fewer items than CUs (batch-1 latency): 3x the workgroups per slot, each
+// with a third of the rows (launch_forward_f16).
+template <int FO_>
+struct P16T {
   using S = _Float16;
   using WT = _Float16;
   using BT = float;
@@ -114,7 +118,7 @@ struct P16 {
   static constexpr int KC = 32;   // channels per K chunk (one MFMA K)
   static constexpr int CPL = 8;   // channels per lane per chunk
   static constexpr int EPC = 8;   // storage elements per 16-byte LDS chunk
-  static constexpr int FO = 24;   // output subcarriers per strip
+  static constexpr int FO = FO_;  // output subcarriers per strip
   static constexpr int R = 4;     // consecutive subcarrier rows per wave pass
   static constexpr bool WLDS = true;  // stage each layer's weights in LDS
   __device__ static DV ld_lds(const char* p) { return *reinterpret_cast<const half8*>(p); }
@@ -160,6 +164,9 @@ struct P16 {
     return __builtin_bit_cast(DV, x);
   }
 };
+
+using P16 = P16T<24>;
+using P16S = P16T<8>;
 
 struct P64 {
   using S = float;
@@ -769,7 +776,7 @@ constexpr int strip_lds_bytes(bool heads_wb = false) {
   return strip_slots<P>() * slot_pitch<P>() + (P::WLDS ? (heads_wb ? kWAlloc : kWBytes) : 0);
 }
 static_assert(strip_lds_bytes<P16>(true) == 160 * 1024, "P16 strip image + WB = LDS");
-static_assert(P16::FO <= 8 * P16::R, "the conv3 of a strip must run in one round");
+static_assert(P16::FO <= 8 * P16::R && P16S::FO <= 8 * P16S::R, "the conv3 of a strip must run in one round");
 
 // in-plane element offset of (f, t) in a [F][14][56] state plane (< 2^31 for F <= 3276)
 __device__ __forceinline__ int sre(int f, int t) { return (f * kT + t) * kDS; }
@@ -792,7 +799,8 @@ __device__ __forceinline__ void run_layer(char* X, char* WB, const SepW<typename
   }
 }
 
-static_assert(P16::FO + 4 <= 8 * P16::R, "P16 layers must run in one round (weights are swapped after it)");
+static_assert(P16::FO + 4 <= 8 * P16::R && P16S::FO + 4 <= 8 * P16S::R,
+              "P16 layers must run in one round (weights are swapped after it)");
 
 // ------------------------------------------------------ dense layers from registers
 // Dense weights: LDS image (P16, staged by the workgroup) or global (P64); K permuted.
@@ -2090,9 +2098,18 @@ struct Launch {
   }
 };
 
+#ifndef NRX_SMALL_STRIPS
+#define NRX_SMALL_STRIPS 1
+#endif
+// Small grids (every 8-row strip gets a CU of its own) run the 8-row strips: the forward
+// is latency-bound there, and a workgroup's time scales with its rows.  The readout
+// heads must fit the smaller strip image (X layout: H LLR heads + ChEst, 25 KB each).
 hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args,
                               const ModelW<_Float16, float>& W, int num_it, hipStream_t st,
                               Prof* prof) {
+  const long items8 = (long)args.B * args.U * ((args.F + P16S::FO - 1) / P16S::FO);
+  const bool heads_fit = (args.H + 1) * (kHeadSlot + 1024) <= strip_slots<P16S>() * slot_pitch<P16S>();
+  if (NRX_SMALL_STRIPS != 0 && items8 <= cu_count() && heads_fit) return Launch<P16S>::run(args, W, num_it, st, prof);
   return Launch<P16>::run(args, W, num_it, st, prof);
 }
 
@@ -2109,8 +2126,9 @@ hipError_t setup_kernels() {
       dev >= 0 && dev < kMaxDevices)
     g_cu_count[dev] = cus;
   hipError_t e = Launch<P16>::setup();
+  hipError_t e1 = Launch<P16S>::setup();
   hipError_t e2 = Launch<P64>::setup();
-  return e != hipSuccess ? e : e2;
+  return e != hipSuccess ? e : (e1 != hipSuccess ? e1 : e2);
 }
 
 int strip_width(int precision) { return precision == 0 ? P16::FO : P64::FO; }
