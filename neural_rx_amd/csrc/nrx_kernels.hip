@@ -104,9 +104,9 @@ __device__ __forceinline__ half2 h2(half8 v, int k) {
   return half2{v[2 * k], v[2 * k + 1]};
 }
 
-// FO_: output subcarriers per strip.  P16 (24) is the throughput shape; P16S (8) is taken
-// for grids with fewer items than CUs (batch-1 latency): 3x the workgroups per slot, each
-// with a third of the rows (launch_forward_f16).
+// FO_: output subcarriers per strip.  P16 (24) is the throughput shape; P16M (16) and P16S
+// (8) are taken for grids that would leave CUs idle (batch-1 latency): more workgroups per
+// slot, each with fewer rows (launch_forward_f16).
 template <int FO_>
 struct P16T {
   using S = _Float16;
@@ -166,6 +166,7 @@ struct P16T {
 };
 
 using P16 = P16T<24>;
+using P16M = P16T<16>;
 using P16S = P16T<8>;
 
 struct P64 {
@@ -776,7 +777,8 @@ constexpr int strip_lds_bytes(bool heads_wb = false) {
   return strip_slots<P>() * slot_pitch<P>() + (P::WLDS ? (heads_wb ? kWAlloc : kWBytes) : 0);
 }
 static_assert(strip_lds_bytes<P16>(true) == 160 * 1024, "P16 strip image + WB = LDS");
-static_assert(P16::FO <= 8 * P16::R && P16S::FO <= 8 * P16S::R, "the conv3 of a strip must run in one round");
+static_assert(P16::FO <= 8 * P16::R && P16M::FO <= 8 * P16M::R && P16S::FO <= 8 * P16S::R,
+              "the conv3 of a strip must run in one round");
 
 // in-plane element offset of (f, t) in a [F][14][56] state plane (< 2^31 for F <= 3276)
 __device__ __forceinline__ int sre(int f, int t) { return (f * kT + t) * kDS; }
@@ -799,7 +801,7 @@ __device__ __forceinline__ void run_layer(char* X, char* WB, const SepW<typename
   }
 }
 
-static_assert(P16::FO + 4 <= 8 * P16::R && P16S::FO + 4 <= 8 * P16S::R,
+static_assert(P16::FO + 4 <= 8 * P16::R && P16M::FO + 4 <= 8 * P16M::R && P16S::FO + 4 <= 8 * P16S::R,
               "P16 layers must run in one round (weights are swapped after it)");
 
 // ------------------------------------------------------ dense layers from registers
@@ -2101,15 +2103,22 @@ struct Launch {
 #ifndef NRX_SMALL_STRIPS
 #define NRX_SMALL_STRIPS 1
 #endif
-// Small grids (every 8-row strip gets a CU of its own) run the 8-row strips: the forward
-// is latency-bound there, and a workgroup's time scales with its rows.  The readout
-// heads must fit the smaller strip image (X layout: H LLR heads + ChEst, 25 KB each).
+// Small grids: the forward is latency-bound and a workgroup's time scales with its rows, so
+// the narrowest strips whose items all get a CU of their own are taken (24-row strips
+// otherwise).  The readout heads must fit the strip image (X layout: H LLR heads + ChEst,
+// 25 KB each).
+template <class P>
+static bool small_strips_fit(const FwdArgs<_Float16, float, _Float16>& a) {
+  const long items = (long)a.B * a.U * ((a.F + P::FO - 1) / P::FO);
+  return items <= cu_count() && (a.H + 1) * (kHeadSlot + 1024) <= strip_slots<P>() * slot_pitch<P>();
+}
 hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args,
                               const ModelW<_Float16, float>& W, int num_it, hipStream_t st,
                               Prof* prof) {
-  const long items8 = (long)args.B * args.U * ((args.F + P16S::FO - 1) / P16S::FO);
-  const bool heads_fit = (args.H + 1) * (kHeadSlot + 1024) <= strip_slots<P16S>() * slot_pitch<P16S>();
-  if (NRX_SMALL_STRIPS != 0 && items8 <= cu_count() && heads_fit) return Launch<P16S>::run(args, W, num_it, st, prof);
+  if (NRX_SMALL_STRIPS != 0) {
+    if (small_strips_fit<P16S>(args)) return Launch<P16S>::run(args, W, num_it, st, prof);
+    if (small_strips_fit<P16M>(args)) return Launch<P16M>::run(args, W, num_it, st, prof);
+  }
   return Launch<P16>::run(args, W, num_it, st, prof);
 }
 
@@ -2127,6 +2136,7 @@ hipError_t setup_kernels() {
     g_cu_count[dev] = cus;
   hipError_t e = Launch<P16>::setup();
   hipError_t e1 = Launch<P16S>::setup();
+  if (e1 == hipSuccess) e1 = Launch<P16M>::setup();
   hipError_t e2 = Launch<P64>::setup();
   return e != hipSuccess ? e : (e1 != hipSuccess ? e1 : e2);
 }

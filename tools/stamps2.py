@@ -30,7 +30,7 @@ from neural_rx_amd.receiver import CGNNEngine, compute_pe  # noqa: E402
 
 cfg = get_config("nrx_rt")
 spec = spec_from_config(cfg)
-B, U, prbs = 128, 2, 4
+B, U, prbs = int(os.environ.get("NRX_STAMP_B", 128)), 2, int(os.environ.get("NRX_STAMP_PRBS", 4))
 sl = synth.generate(B, U, prbs, 4, [4, 4], (0, 1), snr_db=10, seed=3)
 eng = CGNNEngine(spec, W.load("nrx_rt"))
 t = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
