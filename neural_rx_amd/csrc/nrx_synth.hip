@@ -169,35 +169,51 @@ __global__ __launch_bounds__(64) void k_gen_params(nrx_gen_desc d, GenWs w, floa
   }
 }
 
-// one thread per (b, u, a, l, t): g(t) = sqrt(pdp_l) sum_s g0_s exp(j 2 pi fd_s t Tsym)
-// (the sinusoid draws are recomputed per t: 14x more threads instead of a serial t loop of
-// f64 sin/cos per thread, which left this launch latency-bound)
-__global__ __launch_bounds__(256) void k_gen_taps(nrx_gen_desc d, GenWs w) {
-  const int U = d.num_tx, A = d.num_rx_ant, L = d.num_taps, NS = d.num_sinusoids, T = d.num_symbols;
-  const int64_t n = (int64_t)d.batch * U * A * L * T;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const int t = (int)(i % T);
-  const int64_t bual = i / T;
-  const int l = (int)(bual % L);
-  const int a = (int)((bual / L) % A);
-  const int u = (int)((bual / ((int64_t)L * A)) % U);
-  const int64_t b = bual / ((int64_t)L * A * U);
+// g(t) = sqrt(pdp_l) sum_s g0_s exp(j 2 pi fd_s t Tsym).  A block owns kTapGroups
+// (b, u, a, l) groups: the NS sinusoid draws of each group (Philox + Box-Muller + Doppler
+// cosine, the f64 transcendentals) are made once into LDS, then one thread per (group, t)
+// sums the NS rotations -- the same operations per value as drawing them per thread (the
+// taps are unchanged bit for bit) at 1/T of the draw work.
+constexpr int kTapGroups = 16;
+constexpr int kMaxSinusoids = 16;   // nrx_generate_slots validates num_sinusoids <= 16
+
+__global__ __launch_bounds__(kTapGroups * kT) void k_gen_taps(nrx_gen_desc d, GenWs w) {
+  __shared__ double sg[kTapGroups * kMaxSinusoids][3];
+  const int U = d.num_tx, A = d.num_rx_ant, L = d.num_taps, NS = d.num_sinusoids;
+  const int64_t ngrp = (int64_t)d.batch * U * A * L;
+  const int64_t g0 = (int64_t)blockIdx.x * kTapGroups;
   const double tsym = kCP / d.subcarrier_spacing;
   const double sc = 1.0 / sqrt(2.0 * NS);
-  double ar = 0.0, ai = 0.0;
-  for (int s = 0; s < NS; ++s) {
+  for (int j = threadIdx.x; j < kTapGroups * NS; j += kTapGroups * kT) {
+    const int64_t g = g0 + j / NS;
+    const int s = j % NS;
+    if (g >= ngrp) continue;
+    const int l = (int)(g % L);
+    const int a = (int)((g / L) % A);
+    const int u = (int)((g / ((int64_t)L * A)) % U);
+    const int64_t b = g / ((int64_t)L * A * U);
     const U4 r = draw(d, b, ST_TAP, (uint32_t)((((u * A + a) * L + l) * NS) + s));
     const double2 z = box_muller(r.x, r.y);
-    const double g0r = z.x * sc, g0i = z.y * sc;
-    const double fd = d.max_doppler_hz * cos(2.0 * kPi * uni(r.z));
+    sg[j][0] = z.x * sc;
+    sg[j][1] = z.y * sc;
+    sg[j][2] = d.max_doppler_hz * cos(2.0 * kPi * uni(r.z));
+  }
+  __syncthreads();
+  const int gl = threadIdx.x / kT, t = threadIdx.x % kT;
+  const int64_t g = g0 + gl;
+  if (g >= ngrp) return;
+  double ar = 0.0, ai = 0.0;
+  for (int s = 0; s < NS; ++s) {
+    const double g0r = sg[gl * NS + s][0], g0i = sg[gl * NS + s][1], fd = sg[gl * NS + s][2];
     const double ph = 2.0 * kPi * (fd * (t * tsym));
     const double c = cos(ph), sn = sin(ph);
     ar += g0r * c - g0i * sn;
     ai += g0r * sn + g0i * c;
   }
-  const double sp = w.spdp[(b * U + u) * L + l];
-  w.gt[i] = make_double2(ar * sp, ai * sp);
+  const int l = (int)(g % L);
+  const int64_t bu = g / ((int64_t)L * A);
+  const double sp = w.spdp[bu * L + l];
+  w.gt[g * kT + t] = make_double2(ar * sp, ai * sp);
 }
 
 // one thread per (b, u, f, t)
@@ -431,7 +447,7 @@ hipError_t launch_generate(const nrx_gen_desc& d, const nrx_gen_out& o, void* ws
                 L = d.num_taps;
   auto blocks = [](int64_t n) { return (unsigned)((n + 255) / 256); };
   k_gen_params<<<(unsigned)B, 64, 0, st>>>(d, w, o.active, o.mcs_mask, o.mcs);
-  k_gen_taps<<<blocks(B * U * A * L * T), 256, 0, st>>>(d, w);
+  k_gen_taps<<<(unsigned)((B * U * A * L + kTapGroups - 1) / kTapGroups), kTapGroups * kT, 0, st>>>(d, w);
   k_gen_tx<<<blocks(B * U * F * T), 256, 0, st>>>(d, w, o.bits, o.bits_stride);
   const int at = (int)(A * T);
   int FB = 256 / at;
