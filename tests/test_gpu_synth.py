@@ -132,6 +132,29 @@ def test_error_counters_match_oracle(config, var_mcs):
     assert ref[:, 0].sum() > 0                      # 4 dB: errors present
 
 
+@pytest.mark.parametrize("batch,heads,bs", [(100, 1, 4), (2085, 3, 6), (33, 2, 8)])
+def test_error_counters_many_slots(batch, heads, bs):
+    """Workgroups that own several slots (G = 32 slot groups per user) and more than one
+    64-slot pass (batch 2085), per-slot MCS heads, random activity; synthetic LLRs (some
+    exactly 0, which decide 0) against the oracle's counters."""
+    import torch
+    from neural_rx_amd.generator import count_errors
+    rng = np.random.default_rng(batch)
+    U, F, T = 2, 12, 14
+    mcs_bits = [2, 4, 6][:heads] if heads > 1 else [bs if bs <= 6 else 4]
+    llr = rng.standard_normal((heads, batch, U, F, T, bs)).astype(np.float32)
+    llr[rng.random(llr.shape) < 0.05] = 0.0
+    bits = (rng.random((batch, U, F, T, bs)) < 0.5).astype(np.uint8)
+    active = (rng.random((batch, U)) < 0.7).astype(np.float32)
+    mcs = rng.integers(0, len(mcs_bits), (batch, U)).astype(np.uint8)
+    dmrs = [2, 11]
+    t = lambda a: torch.from_numpy(a).cuda()
+    counts = count_errors(t(llr), t(bits), t(active), t(mcs), mcs_bits, dmrs)
+    torch.cuda.synchronize()
+    ref = S.count_errors(llr, bits, mcs, mcs_bits, active, dmrs)
+    np.testing.assert_array_equal(counts.cpu().numpy(), ref)
+
+
 def test_sim_ber_loop():
     from neural_rx_amd import weights as W
     from neural_rx_amd.evaluate import sim_ber
