@@ -416,6 +416,110 @@ __global__ __launch_bounds__(256) void k_count_errors(nrx_count_io c, int G) {
   }
 }
 
+// Same counters for the common LLR widths (bits_stride 2, 4, 6, 8), one (slot, RE) unit
+// per thread: a workgroup (g, u) walks the units of its slots as one flat index space,
+// kCntUnroll units per thread per step with every load issued unconditionally (clamped
+// index, masked afterwards) before any compare; per-slot bit errors gather in LDS.  nrx_rt,
+// 128 slots: 10.2 us vs 13.4 us for the slot loop above.  Measured flat in the layout
+// (profiles/r02/ab_count_errors.txt): 4 or 12 units per step, G = 8 / 16 / 32 slot groups
+// of 1024 / 512 / 256 threads all 9.5-11.7 us; G = 128 (four times the same-address int64
+// atomics) 16.4 us.
+#ifndef NRX_CNT_UNROLL
+#define NRX_CNT_UNROLL 4
+#endif
+#ifndef NRX_CNT_T
+#define NRX_CNT_T 256
+#endif
+#ifndef NRX_CNT_G
+#define NRX_CNT_G 32
+#endif
+constexpr int kCntSlots = 64;
+constexpr int kCntUnroll = NRX_CNT_UNROLL;
+
+template <int BSC>
+__global__ __launch_bounds__(NRX_CNT_T) void k_count_errors_re(nrx_count_io c, int G) {
+  __shared__ unsigned s_err[kCntSlots];
+  __shared__ int s_nb[kCntSlots];          // bits of the slot's MCS, 0 when the user is inactive
+  __shared__ long long s_l[kCntSlots];     // element offset of the slot's LLR grid (its head)
+  __shared__ long long s_b[kCntSlots];     // element offset of the slot's bit grid
+  const int U = c.num_tx, F = c.num_subcarriers, T = c.num_symbols;
+  const int u = blockIdx.y;
+  const int FT = F * T;
+  unsigned long long err_tot = 0, bits_tot = 0, blk_err = 0, blks = 0;
+  int ndata = 0;
+  for (int t = 0; t < T; ++t) ndata += !((c.dmrs_symbol_mask >> t) & 1);
+  const int nslots = (c.batch - (int)blockIdx.x + G - 1) / G;
+  for (int j0 = 0; j0 < nslots; j0 += kCntSlots) {
+    const int nj = nslots - j0 < kCntSlots ? nslots - j0 : kCntSlots;
+    if ((int)threadIdx.x < nj) {
+      const long long bu = (long long)((int)blockIdx.x + G * (j0 + (int)threadIdx.x)) * U + u;
+      int nb = 0, head = 0;
+      if (c.active[bu] > 0.0f) {
+        const int m = c.mcs ? c.mcs[bu] : 0;
+        nb = c.mcs_bits[m];
+        head = c.num_heads > 1 ? m : 0;
+      }
+      s_nb[threadIdx.x] = nb;
+      s_l[threadIdx.x] = ((long long)head * c.batch * U + bu) * FT * BSC;
+      s_b[threadIdx.x] = bu * FT * BSC;
+      s_err[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const int n = nj * FT;
+    for (int e0 = 0; e0 < n; e0 += NRX_CNT_T * kCntUnroll) {
+      float lv[kCntUnroll][BSC];
+      uint8_t sv[kCntUnroll][BSC];
+      int jl[kCntUnroll], ii[kCntUnroll];
+#pragma unroll
+      for (int q = 0; q < kCntUnroll; ++q) {
+        int e = e0 + q * NRX_CNT_T + (int)threadIdx.x;
+        e = e < n ? e : n - 1;
+        jl[q] = e / FT;
+        ii[q] = e - jl[q] * FT;
+        const float* lp = c.llr + s_l[jl[q]] + (long long)ii[q] * BSC;
+        const uint8_t* bp = c.bits + s_b[jl[q]] + (long long)ii[q] * BSC;
+#pragma unroll
+        for (int k = 0; k < BSC; ++k) {
+          lv[q][k] = lp[k];
+          sv[q][k] = bp[k];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kCntUnroll; ++q) {
+        const int e = e0 + q * NRX_CNT_T + (int)threadIdx.x;
+        const int nb = s_nb[jl[q]];
+        if (e >= n || !nb || ((c.dmrs_symbol_mask >> (ii[q] % T)) & 1)) continue;
+        unsigned er = 0;
+#pragma unroll
+        for (int k = 0; k < BSC; ++k) er += (k < nb && (uint8_t)(lv[q][k] > 0.0f) != sv[q][k]) ? 1u : 0u;
+        if (er) atomicAdd(&s_err[jl[q]], er);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int j = 0; j < nj; ++j) {
+        if (!s_nb[j]) continue;
+        err_tot += s_err[j];
+        bits_tot += (unsigned long long)ndata * F * s_nb[j];
+        blk_err += s_err[j] ? 1 : 0;
+        blks += 1;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && blks) {
+    unsigned long long* o = reinterpret_cast<unsigned long long*>(c.counts) + 4 * u;
+#ifdef NRX_CNT_NOATOM
+    if (err_tot == 12345678) o[0] = 0;
+#else
+    atomicAdd(o + 0, err_tot);
+    atomicAdd(o + 1, bits_tot);
+    atomicAdd(o + 2, blk_err);
+    atomicAdd(o + 3, blks);
+#endif
+  }
+}
+
 size_t al(size_t x) { return (x + 255) / 256 * 256; }
 
 }  // namespace
@@ -462,8 +566,19 @@ hipError_t launch_generate(const nrx_gen_desc& d, const nrx_gen_out& o, void* ws
 }
 
 hipError_t launch_count_errors(const nrx_count_io& c, hipStream_t st) {
-  const int G = c.batch < 32 ? c.batch : 32;
-  k_count_errors<<<dim3(G, c.num_tx), 256, 0, st>>>(c, G);
+  const int G = c.batch < NRX_CNT_G ? c.batch : NRX_CNT_G;
+  const dim3 grid(G, c.num_tx);
+  switch (c.bits_stride) {
+    case 2: k_count_errors_re<2><<<grid, NRX_CNT_T, 0, st>>>(c, G); break;
+    case 4: k_count_errors_re<4><<<grid, NRX_CNT_T, 0, st>>>(c, G); break;
+    case 6: k_count_errors_re<6><<<grid, NRX_CNT_T, 0, st>>>(c, G); break;
+    case 8: k_count_errors_re<8><<<grid, NRX_CNT_T, 0, st>>>(c, G); break;
+    default: {
+      const int G32 = c.batch < 32 ? c.batch : 32;
+      k_count_errors<<<dim3(G32, c.num_tx), 256, 0, st>>>(c, G32);
+    }
+  }
+
   return hipGetLastError();
 }
 

@@ -132,7 +132,7 @@ def test_error_counters_match_oracle(config, var_mcs):
     assert ref[:, 0].sum() > 0                      # 4 dB: errors present
 
 
-@pytest.mark.parametrize("batch,heads,bs", [(100, 1, 4), (2085, 3, 6), (33, 2, 8)])
+@pytest.mark.parametrize("batch,heads,bs", [(100, 1, 4), (2085, 3, 6), (33, 2, 8), (50, 1, 2), (40, 1, 5)])
 def test_error_counters_many_slots(batch, heads, bs):
     """Workgroups that own several slots (G = 32 slot groups per user) and more than one
     64-slot pass (batch 2085), per-slot MCS heads, random activity; synthetic LLRs (some
