@@ -913,6 +913,10 @@ __device__ __forceinline__ int head_w2(int h) { return head_w1(h) + 16 * 1024; }
 __device__ __forceinline__ int head_b1(int h) { return head_w1(h) + kHeadSlot; }
 __device__ __forceinline__ int head_b2(int h) { return head_b1(h) + 512; }
 
+#ifndef NRX_RO_STRAIGHT
+#define NRX_RO_STRAIGHT 1
+#endif
+
 // conv3 epilogue: new state rows (+ aggregation MLP or readouts) for the R rows of a
 // wave.  All R rows are computed unconditionally (rows past the strip or the grid hold
 // finite values from zero inputs) so the MLP chains of the rows interleave; only the
@@ -1198,9 +1202,9 @@ struct EpiConv3 {
         CFrag<P, NTS> sbr[RB];
 #pragma unroll
         for (int r = 0; r < RB; ++r) sbr[r] = sb[r0 + r];
-        for (int hh = 0; hh <= a.H; ++hh) {
-          const bool ch = hh == a.H;
-          if (ch && !a.h_ref) break;
+        // one head (hh < H: LLR head hh, hh == H: ChEst); straight-line for the common
+        // single LLR head so the ChEst MFMAs can start under the LLR head's tail
+        auto one_head = [&](int hh, bool ch) __attribute__((always_inline)) {
           if (!ch) {
             Real o[RB][1][4];
             if constexpr (P::WLDS) {
@@ -1251,6 +1255,16 @@ struct EpiConv3 {
               const int f = f_start + p0 + r0 + r;
               store_f32<CHP / 16>(a.h_ref + ((((size_t)b * U + u) * F + f) * kT + t) * A2, o[r], g, A2);
             }
+          }
+        };
+        if (NRX_RO_STRAIGHT && a.H == 1) {
+          one_head(0, false);
+          if (a.h_ref) one_head(1, true);
+        } else {
+          for (int hh = 0; hh <= a.H; ++hh) {
+            const bool ch = hh == a.H;
+            if (ch && !a.h_ref) break;
+            one_head(hh, ch);
           }
         }
       }
