@@ -1580,6 +1580,13 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
   stamp(4);
 }
 
+// Waves that issue the paired next item's z DMA (0 .. NW-1; 8: all).  A burst of LDS-DMA
+// issues stalls the issuing wave; with NW = 4 one wave of each SIMD pair issues while the
+// other runs its epilogue.
+#ifndef NRX_DMA_NW
+#define NRX_DMA_NW 4
+#endif
+
 // 16 zero bytes: the LDS-DMA source of every z chunk that is zero (pad symbols, rows
 // outside the grid, channel padding, the missing other user of U = 1)
 __device__ intx4 g_zero16[1];
@@ -1596,7 +1603,7 @@ __device__ intx4 g_zero16[1];
 // chunks of one slot); the chunk swizzle is applied on the source address (the lane at
 // physical chunk q' of symbol t loads logical chunk q' ^ swz(t)).  The pe chunk (2 values)
 // is written by ds_write after the DMA has landed.
-template <class P>
+template <class P, int NW = 8>
 __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X, int b, int u, int f_start) {
   using S = typename P::S;
   static_assert(sizeof(S) == 2 && kUPD_CINP * 2 / 16 == 16, "f16 z image with 16 chunks per symbol row");
@@ -1625,7 +1632,8 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
       lsrc = sp + t * kDS + P::EPC * (q - QS);
     }
   }
-  for (int k = wave; k < R0 * 4; k += 8) {
+  if (wave >= NW) return;
+  for (int k = wave; k < R0 * 4; k += NW) {
     const int f = f_start + (k >> 2);             // wave-uniform
     const S* src = reinterpret_cast<const S*>(g_zero16);
     if (f >= 0 && f < F && lsrc) src = lsrc + (size_t)f * (kT * kDS);
@@ -1635,7 +1643,7 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
 
 template <class P, class WS, int CHP, int TAILM>
 __device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook() const {
-  if constexpr (kNextHook || kNextHookRO) zload_dma_u2<P>(*prm, X, nb, nu, nfs);
+  if constexpr (kNextHook || kNextHookRO) zload_dma_u2<P, NRX_DMA_NW>(*prm, X, nb, nu, nfs);
 }
 
 // Rest of an update item whose z image is being filled by LDS-DMA (issued by the caller, or
