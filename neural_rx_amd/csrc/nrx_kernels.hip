@@ -1651,7 +1651,7 @@ __device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook() const {
 // block.  (nb, nu, nfs): the next item of a paired workgroup (nb < 0: none).
 template <class P, int CHP, int TAILM>
 __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X, char* WB, int b, int u, int f_start,
-                                             int nb, int nu, int nfs) {
+                                             int nb, int nu, int nfs, bool issue_z = false) {
   using S = typename P::S;
   constexpr int R0 = strip_slots<P>();
   constexpr int NQ = kUPD_CINP * (int)sizeof(S) / 16;
@@ -1665,6 +1665,9 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
   const bool pe_ok = pe_slot < R0 && pe_f >= 0 && pe_f < F;
   const float2 pe_v = *reinterpret_cast<const float2*>(
       a.pe + (((size_t)u * F + (pe_ok ? pe_f : 0)) * kT + (pe_ok ? pe_t : 0)) * 2);
+  // first item of a workgroup: its z DMA goes out behind the conv1-weight and pe loads, so
+  // their latency hides under the DMA instead of following it
+  if (issue_z) zload_dma_u2<P>(prm, X, b, u, f_start);
   stamp(24);
   stamp(25);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1688,6 +1691,9 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
 #ifndef NRX_PAIR
 #define NRX_PAIR 1
 #endif
+#ifndef NRX_W1_FIRST
+#define NRX_W1_FIRST 1
+#endif
 #ifndef NRX_PAIR_RO
 #define NRX_PAIR_RO 1
 #endif
@@ -1702,8 +1708,8 @@ __device__ __forceinline__ void update_pair(const BlockParams<P>& prm, char* sme
   char* X = smem;
   char* WB = smem + R0 * slot_pitch<P>();
   const int fs0 = s0 * P::FO - kHalo, fs1 = s1 * P::FO - kHalo;
-  zload_dma_u2<P>(prm, X, b0, u0, fs0);
-  dma_item_run<P, CHP, TAILM>(prm, X, WB, b0, u0, fs0, b1, u1, fs1);
+  if (!NRX_W1_FIRST) zload_dma_u2<P>(prm, X, b0, u0, fs0);
+  dma_item_run<P, CHP, TAILM>(prm, X, WB, b0, u0, fs0, b1, u1, fs1, NRX_W1_FIRST != 0);
   dma_item_run<P, CHP, TAILM>(prm, X, WB, b1, u1, fs1, -1, 0, 0);
 }
 
@@ -1722,8 +1728,8 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
   char* WB = smem + R0 * slot_pitch<P>();
   if constexpr (sizeof(S) == 2 && NRX_ZDMA != 0) {
     if (prm.inline_combine && U <= 2) {
-      zload_dma_u2<P>(prm, X, b, u, f_start);
-      dma_item_run<P, CHP, TAILM>(prm, X, WB, b, u, f_start, -1, 0, 0);
+      if (!NRX_W1_FIRST) zload_dma_u2<P>(prm, X, b, u, f_start);
+      dma_item_run<P, CHP, TAILM>(prm, X, WB, b, u, f_start, -1, 0, 0, NRX_W1_FIRST != 0);
       return;
     }
   }
