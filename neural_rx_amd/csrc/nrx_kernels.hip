@@ -1457,6 +1457,10 @@ __global__ __launch_bounds__(1024) void k_norm(const float* __restrict__ y, int 
   }
 }
 
+#ifndef NRX_INIT_ORDER
+#define NRX_INIT_ORDER 1
+#endif
+
 // slot grids above this many float4s get the separate k_norm pass (nrx_rt: 1 344)
 constexpr int kNormFusedMaxQ = 8192;
 
@@ -1475,17 +1479,25 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
   const int f_start = f0 - kHalo;
   char* X = smem;
   char* WB = smem + R0 * slot_pitch<P>();
-  if constexpr (sizeof(S) == 2 && CINP < kHID) {
-    // pad symbols t = 14, 15 of the 128-channel layout the conv layers write in place:
-    // zero once (the z image below occupies the first CINP*32 bytes of each slot)
-    constexpr int NQ = kHID * (int)sizeof(S) / 16;
-    for (int idx = threadIdx.x; idx < R0 * 2 * NQ; idx += 512) {
-      const int q = idx % NQ, tt = kT + (idx / NQ) % 2, lf = idx / (2 * NQ);
-      *reinterpret_cast<intx4*>(X + xoff<P, NQ>(lf, tt, q)) = intx4{0, 0, 0, 0};
+  auto pad_zero = [&]() __attribute__((always_inline)) {
+    if constexpr (sizeof(S) == 2 && CINP < kHID) {
+      // pad symbols t = 14, 15 of the 128-channel layout the conv layers write in place:
+      // zero once (the z image below occupies the first CINP*32 bytes of each slot; its
+      // own t = 14, 15 stores are zeros too, so the two may land in either order)
+      constexpr int NQ = kHID * (int)sizeof(S) / 16;
+      for (int idx = threadIdx.x; idx < R0 * 2 * NQ; idx += 512) {
+        const int q = idx % NQ, tt = kT + (idx / NQ) % 2, lf = idx / (2 * NQ);
+        *reinterpret_cast<intx4*>(X + xoff<P, NQ>(lf, tt, q)) = intx4{0, 0, 0, 0};
+      }
     }
-  }
+  };
   SepStage<CINP, kHID> w1;
-  if constexpr (P::WLDS) w1.load(prm.w[0]);
+  // NRX_INIT_ORDER: the y / h / pe loads (the norm -> z chain) go out first; the conv1
+  // weights and the pad zeroing follow them
+  if (!NRX_INIT_ORDER) {
+    pad_zero();
+    if constexpr (P::WLDS) w1.load(prm.w[0]);
+  }
   // small grids: the slot norm's y loads go out first, beside the z-row loads below
   const float* yslot = a.y + (size_t)b * F * kT * A2;
   const int nqs = F * kT * A2 / 4;
@@ -1549,6 +1561,10 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
     float2 pv = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + (ok ? f : 0)) * kT + (ok ? tt : 0)) * 2);
     if (!ok) pv = float2{0.f, 0.f};
     stamp(33);
+    if (NRX_INIT_ORDER) {
+      if constexpr (P::WLDS) w1.load(prm.w[0]);
+      pad_zero();
+    }
     // large grids: the per-slot k_norm pass already reduced y (every workgroup of the slot
     // re-reading the whole grid costs O(strips x grid) there); small grids: fused here
     const Real ns = prm.norm_pre ? (Real)a.norm[b] : (Real)slot_norm(npre, yslot, nqs, red);
