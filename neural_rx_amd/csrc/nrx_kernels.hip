@@ -1602,6 +1602,9 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
 #ifndef NRX_DMA_NW
 #define NRX_DMA_NW 4
 #endif
+#ifndef NRX_DMA_HI
+#define NRX_DMA_HI 0
+#endif
 
 // 16 zero bytes: the LDS-DMA source of every z chunk that is zero (pad symbols, rows
 // outside the grid, channel padding, the missing other user of U = 1)
@@ -1648,8 +1651,11 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
       lsrc = sp + t * kDS + P::EPC * (q - QS);
     }
   }
-  if (wave >= NW) return;
-  for (int k = wave; k < R0 * 4; k += NW) {
+  // NRX_DMA_HI: the last NW waves issue instead of the first (same per-lane sources:
+  // the symbol group is wave & 3 either way)
+  const int w0 = NRX_DMA_HI ? 8 - NW : 0;
+  if (wave < w0 || wave >= w0 + NW) return;
+  for (int k = wave - w0; k < R0 * 4; k += NW) {
     const int f = f_start + (k >> 2);             // wave-uniform
     const S* src = reinterpret_cast<const S*>(g_zero16);
     if (f >= 0 && f < F && lsrc) src = lsrc + (size_t)f * (kT * kDS);
