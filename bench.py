@@ -15,7 +15,8 @@ all-reduce of the per-rank elapsed time (MAX) after the timed region.
 Prints ONE JSON line (rank 0) with the headline metric (slots/s, whole job), the
 per-slot p50 latency at batch 1, the roofline of the dominant kernel
 (state update, measured with HIP events on the launch stream) and a CPU baseline
-(the numpy oracle, fp32, timed on a bounded sample on this host).
+(the torch-CPU restatement, fp32, BASELINE.md's plan: cfg1 latency and cfg2 throughput at
+all threads and at 1 thread, on a bounded sample on this host).
 """
 from __future__ import annotations
 
@@ -181,14 +182,19 @@ def main():
     peak = metrics.PEAK_TFLOPS[args.precision]
     achieved = dom_flops / dom_avg_s / 1e12
     traffic = None
+    pmc, key = {}, f"{args.config}_b{B}_u{U}_p{args.prbs}_{args.precision}"
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
-            key = f"{args.config}_b{B}_u{U}_p{args.prbs}_{args.precision}"
             traffic = pmc.get(key, {}).get("k_update_bytes_per_launch")
         except Exception:
             traffic = None
+    pmc_src = None
+    if traffic is not None:
+        pmc_src = pmc.get(key, {}).get("source")
+    whole_tflops = metrics.forward_flops_per_re_user(spec, num_it) * re_users * world / (elapsed / args.steps) / 1e12
+    mixed = metrics.mixed_bound_tflops(spec, num_it, peak) if args.precision == "f16" else None
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "kernel": "k_update (3 sep-convs + fused aggregation/readout tail)",
@@ -197,9 +203,18 @@ def main():
                     spec, num_it, 2 if args.precision == "f16" else 4) * re_users),
                 "avg_launch_us": round(dom_avg_s * 1e6, 3),
                 "avg_launch_us_event_pairs": kern[dom]["avg_us_event_pairs"],
+                "avg_launch_us_kind": "derived: event-pair share of a step x uninstrumented step time",
+                "event_pair_scale": round(scale, 5),
+                "uninstrumented_step_ms": round(stream_step_ms, 5),
                 "timing": "per-launch HIP event pairs give each kernel's share of a step; "
-                          "shares x the uninstrumented step time (HIP events, same stream)"}
-    whole_tflops = metrics.forward_flops_per_re_user(spec, num_it) * re_users * world / (elapsed / args.steps) / 1e12
+                          "shares x the uninstrumented step time (HIP events, same stream)",
+                "whole_forward_tflops": round(whole_tflops, 2),
+                "whole_forward_frac": round(whole_tflops / world / peak, 4),
+                "mixed_bound_tflops": round(mixed, 1) if mixed else None,
+                "frac_of_mixed_bound": round(achieved / mixed, 4) if mixed else None,
+                "mixed_bound_note": "k_update's depthwise FLOPs at the VALU peak (157 TF) + its dense FLOPs "
+                                    "at the f16 MFMA peak, pipes overlapped (metrics.mixed_bound_tflops)",
+                "traffic_source": pmc_src}
 
     # ---- batch-1 per-slot latency (hipGraph replay; device-only and H2D+compute+D2H)
     latency = None
@@ -404,31 +419,67 @@ def measure_latency_aerial(torch, eng, spec, cfg, args, groups, dev, num_it, prb
             "batch1_slots_per_s_e2e": round(1e3 / float(np.median(e2e)), 1)}
 
 
-def cpu_baseline(spec, cfg, slots, pe_np, args, num_it):
-    from oracle import cgnn_ref
-    from neural_rx_amd import weights as W
+def _cpu_model():
     try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:
-        threads = 1
-    w = cgnn_ref.split_keras_weights(W.load(cfg.label), spec)
-    nb = min(4, slots.y.shape[0])
-    y, h, a = slots.y[:nb], slots.h_hat[:nb], slots.active[:nb]
-    done = 0
-    t0 = time.perf_counter()
-    while True:
-        cgnn_ref.cgnn_forward(y, pe_np, h, a, np.ones((nb, a.shape[1], 1), np.float32), w, spec,
-                              num_it=num_it, dtype=np.float32)
-        done += nb
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds:
-            break
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
     import platform
-    return {"value": round(done / el, 2), "unit": "slots/s", "cores": threads, "kind": "port",
-            "sample": f"numpy fp32 oracle (oracle/cgnn_ref.py), {done} slots of the bench workload "
-                      f"({nb}-slot batches, {args.users} users, {args.prbs} PRB) in {el:.1f} s; "
-                      f"BLAS threads={threads}; cpu={platform.processor() or platform.machine()}"}
+    return platform.processor() or platform.machine()
+
+
+def cpu_baseline(spec, cfg, slots, pe_np, args, num_it):
+    """BASELINE.md's CPU-baseline plan: the torch-CPU restatement of the CGNN
+    (oracle/cgnn_torch.py: conv2d(groups=C) depthwise + 1x1 conv, fp32) on this host, at
+    cfg 1 (1 UE, B = 1: p50 latency) and cfg 2 (the bench workload, B = 128: slots/s),
+    with all the threads torch uses here and with 1 thread.  Identical seeded inputs to
+    the GPU run.  The reference's own TF-CPU path cannot run (TensorFlow/Sionna absent)."""
+    import torch
+    from oracle import cgnn_ref
+    from oracle.cgnn_torch import TorchCGNN
+    from neural_rx_amd import synth
+    from neural_rx_amd import weights as W
+    from neural_rx_amd.config import dmrs_symbols, user_cdm_groups
+    from neural_rx_amd.receiver import compute_pe
+    model = TorchCGNN(cgnn_ref.split_keras_weights(W.load(cfg.label), spec), spec)
+    all_threads = torch.get_num_threads()
+    B, U = slots.y.shape[0], slots.h_hat.shape[1]
+    ones = lambda b, u: np.ones((b, u, spec.num_mcs), np.float32)
+    # cfg 1: one user, batch 1 (same trained weights, 4 PRB)
+    g1 = user_cdm_groups(cfg, 1)
+    s1 = synth.generate(1, 1, args.prbs, spec.num_rx_ant, [spec.bits[0]], g1, dmrs_symbols(cfg), snr_db=10.0, seed=1235)
+    pe1 = compute_pe(1, 12 * args.prbs, dmrs_symbols(cfg), g1)
+
+    def p50_b1(n):
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            model.forward(s1.y, pe1, s1.h_hat, s1.active, ones(1, 1), num_it)
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts[2:])) * 1e3
+
+    def b128(reps):
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            model.forward(slots.y, pe_np, slots.h_hat, slots.active, ones(B, U), num_it)
+        return B * reps / (time.perf_counter() - t0)
+
+    res = {}
+    for tag, th in (("all", all_threads), ("1thread", 1)):
+        torch.set_num_threads(th)
+        res[tag] = {"threads": th, "cfg1_b1_p50_ms": round(p50_b1(40 if th > 1 else 25), 3),
+                    "cfg2_b128_slots_per_s": round(b128(2 if th > 1 else 1), 2)}
+    torch.set_num_threads(all_threads)
+    return {"value": res["all"]["cfg2_b128_slots_per_s"], "unit": "slots/s", "cores": all_threads,
+            "kind": "port",
+            "sample": f"torch-CPU fp32 restatement (oracle/cgnn_torch.py), bench workload cfg2 "
+                      f"({B} slots, {U} users, {args.prbs} PRB, num_it {num_it}) x2 batches at {all_threads} threads "
+                      f"(value), plus cfg1 (1 UE, B=1) p50 latency and 1-thread runs",
+            "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+            "all_threads": res["all"], "one_thread": res["1thread"]}
 
 
 if __name__ == "__main__":

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NRX_API_VERSION 3
+#define NRX_API_VERSION 4
 
 enum nrx_status {
   NRX_OK = 0,
@@ -117,6 +117,26 @@ int nrx_forward(nrx_handle* h, const nrx_io* io, void* workspace, size_t workspa
                 void* stream);
 
 void nrx_destroy(nrx_handle* h);
+
+/* Input layouts of y for nrx_forward_ex (the wrappers' own input tensors, so that a
+ * wrapper call launches only libnrx kernels: no host-framework transpose/concat). */
+enum nrx_y_layout {
+  NRX_Y_CGNN = 0,       /* io->y [B][F][T][2A] f32, as nrx_forward */
+  NRX_Y_SIONNA_RG = 1,  /* io->y = the resource grid [B][1][A][T][F] complex64 (re, im
+                           interleaved floats), as CGNNOFDM.forward receives it
+                           (neural_rx.py:813-833: y[:,0].permute(0,3,2,1), cat(real, imag)) */
+  NRX_Y_SPLIT = 2       /* io->y = rx_slot_real [B][F][T][A], y_imag = rx_slot_imag, as
+                           NeuralReceiverONNX.forward (neural_rx.py:1787) */
+};
+
+/* Workspace of nrx_forward_ex: nrx_workspace_size plus the CGNN-layout copy of y. */
+int nrx_workspace_size_ex(const nrx_handle* h, const nrx_shape* shape, int32_t precision, int32_t y_layout,
+                          size_t* bytes);
+
+/* nrx_forward with y in one of the layouts above (y_imag: NRX_Y_SPLIT only, else NULL).
+ * The other tensors of `io` keep their nrx_forward layouts. */
+int nrx_forward_ex(nrx_handle* h, const nrx_io* io, int32_t y_layout, const float* y_imag, void* workspace,
+                   size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- Aerial contract
  * The NeuralReceiverONNX / TensorRT engine I/O (neural_rx.py:1773-1812; feed dict of

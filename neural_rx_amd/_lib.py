@@ -25,7 +25,10 @@ EXPORTS = [
     "nrx_compute_pe", "nrx_flops_per_re_user", "nrx_last_error", "nrx_api_version",
     "nrx_profile_enable", "nrx_profile_read", "nrx_aerial_workspace_size", "nrx_forward_aerial",
     "nrx_llr_demap", "nrx_gen_workspace_size", "nrx_generate_slots", "nrx_count_errors",
+    "nrx_workspace_size_ex", "nrx_forward_ex",
 ]
+# enum nrx_y_layout
+Y_LAYOUTS = {"cgnn": 0, "sionna": 1, "split": 2}
 KERNELS = ["norm", "state_init", "state_update"]
 
 
@@ -196,6 +199,11 @@ def load(path: str = LIB_PATH):
     lib.nrx_workspace_size.restype = c.c_int
     lib.nrx_forward.argtypes = [c.c_void_p, P(nrx_io), c.c_void_p, c.c_size_t, c.c_void_p]
     lib.nrx_forward.restype = c.c_int
+    lib.nrx_workspace_size_ex.argtypes = [c.c_void_p, P(nrx_shape), c.c_int32, c.c_int32, P(c.c_size_t)]
+    lib.nrx_workspace_size_ex.restype = c.c_int
+    lib.nrx_forward_ex.argtypes = [c.c_void_p, P(nrx_io), c.c_int32, c.c_void_p, c.c_void_p, c.c_size_t,
+                                   c.c_void_p]
+    lib.nrx_forward_ex.restype = c.c_int
     lib.nrx_destroy.argtypes = [c.c_void_p]
     lib.nrx_destroy.restype = None
     lib.nrx_compute_pe.argtypes = [c.c_int32, c.c_int32, c.c_int32, P(c.c_int32), c.c_int32,

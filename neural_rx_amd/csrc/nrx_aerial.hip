@@ -200,4 +200,40 @@ hipError_t launch_aerial_llr(const float* llr, int B, int U, int F, int T, int b
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------ y input layouts
+// CGNN channel order [Re a0..a(A-1), Im a0..a(A-1)] from the wrappers' input layouts:
+//   layout 1: Sionna resource grid y[B][1][A][T][F] complex64 (CGNNOFDM.forward,
+//             neural_rx.py:831-833: y[:,0].permute(0,3,2,1), cat(real, imag))
+//   layout 2: split rx_slot_real / rx_slot_imag [B][F][T][A] (NeuralReceiverONNX.forward,
+//             neural_rx.py:1787: cat([y_real, y_imag], -1))
+// One thread per (b, t, f), f fastest: the complex grid is read coalesced along F.
+__global__ __launch_bounds__(256) void k_y_layout(const float* __restrict__ y0, const float* __restrict__ y1,
+                                                  int layout, int F, int T, int A, float* __restrict__ y) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= F * T) return;
+  const int t = i / F, f = i % F;
+  float* o = y + (((size_t)b * F + f) * T + t) * 2 * A;
+  if (layout == 1) {
+    const float2* g = reinterpret_cast<const float2*>(y0) + (size_t)b * A * T * F + (size_t)t * F + f;
+    for (int a = 0; a < A; ++a) {
+      const float2 v = g[(size_t)a * T * F];
+      o[a] = v.x;
+      o[A + a] = v.y;
+    }
+  } else {
+    const size_t q = (((size_t)b * F + f) * T + t) * A;
+    for (int a = 0; a < A; ++a) {
+      o[a] = y0[q + a];
+      o[A + a] = y1[q + a];
+    }
+  }
+}
+
+hipError_t launch_y_layout(const float* y0, const float* y1, int layout, int B, int F, int T, int A, float* y,
+                           hipStream_t st) {
+  k_y_layout<<<dim3((F * T + 255) / 256, B), 256, 0, st>>>(y0, y1, layout, F, T, A, y);
+  return hipGetLastError();
+}
+
 }  // namespace nrx

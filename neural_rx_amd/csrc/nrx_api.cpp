@@ -489,6 +489,43 @@ int nrx_forward(nrx_handle* h, const nrx_io* io, void* workspace, size_t workspa
   return NRX_OK;
 }
 
+static size_t y_cgnn_bytes(const nrx_handle* h, const nrx_shape* s) {
+  return align256((size_t)s->batch * s->num_subcarriers * s->num_symbols * 2 * h->desc.num_rx_ant * sizeof(float));
+}
+
+int nrx_workspace_size_ex(const nrx_handle* h, const nrx_shape* shape, int32_t precision, int32_t y_layout,
+                          size_t* bytes) {
+  int rc = nrx_workspace_size(h, shape, precision, bytes);
+  if (rc) return rc;
+  if (y_layout < NRX_Y_CGNN || y_layout > NRX_Y_SPLIT) return fail(NRX_ERR_INVALID_ARG, "unknown y layout");
+  if (y_layout != NRX_Y_CGNN) *bytes += y_cgnn_bytes(h, shape);
+  return NRX_OK;
+}
+
+int nrx_forward_ex(nrx_handle* h, const nrx_io* io, int32_t y_layout, const float* y_imag, void* workspace,
+                   size_t workspace_bytes, void* stream) {
+  if (!h || !io) return fail(NRX_ERR_INVALID_ARG, "null argument");
+  if (y_layout == NRX_Y_CGNN) {
+    if (y_imag) return fail(NRX_ERR_INVALID_ARG, "y_imag is only used with NRX_Y_SPLIT");
+    return nrx_forward(h, io, workspace, workspace_bytes, stream);
+  }
+  size_t need = 0;
+  int rc = nrx_workspace_size_ex(h, &io->shape, io->precision, y_layout, &need);
+  if (rc) return rc;
+  if (!workspace || workspace_bytes < need)
+    return fail(NRX_ERR_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes");
+  if (!io->y || ((y_layout == NRX_Y_SPLIT) != (y_imag != nullptr)))
+    return fail(NRX_ERR_INVALID_ARG, "y / y_imag do not match the y layout");
+  const size_t yb = y_cgnn_bytes(h, &io->shape);
+  float* ycg = (float*)workspace;
+  hipError_t e = launch_y_layout(io->y, y_imag, y_layout, io->shape.batch, io->shape.num_subcarriers,
+                                 io->shape.num_symbols, h->desc.num_rx_ant, ycg, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "y layout launch");
+  nrx_io cio = *io;
+  cio.y = ycg;
+  return nrx_forward(h, &cio, (char*)workspace + yb, workspace_bytes - yb, stream);
+}
+
 // ---------------------------------------------------------------- Aerial contract
 namespace {
 struct AerialWs {

@@ -92,6 +92,8 @@ hipError_t launch_aerial_tables(const int32_t* ofdm_pos, const int32_t* sc_pos, 
 hipError_t launch_aerial_inputs(const float* y_re, const float* y_im, const float* h_re, const float* h_im,
                                 const int32_t* nn, int B, int U, int F, int T, int A, int nsym, int npil, float* y,
                                 float* h, hipStream_t st);
+hipError_t launch_y_layout(const float* y0, const float* y1, int layout, int B, int F, int T, int A, float* y,
+                           hipStream_t st);
 hipError_t launch_aerial_llr(const float* llr, int B, int U, int F, int T, int bits_max, int bits, float* out,
                              hipStream_t st);
 

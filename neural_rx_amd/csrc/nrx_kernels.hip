@@ -282,8 +282,12 @@ constexpr int kHW1C = 16 * 1024;                 // ChEst W1^T (LLR W1^T at 0)
 constexpr int kHB1 = 32 * 1024;                  // b1: LLR [128] f32, ChEst [128] f32
 constexpr int kHB2 = kHB1 + 2 * kHID * 4;        // b2: LLR [16] f32, ChEst [<= 32] f32
 constexpr int kHW2 = kHB2 + (16 + 32) * 4;       // LLR W2^T rows [bits], then ChEst rows [2A]
-__host__ __device__ constexpr bool heads_fit_wb(int bits_max, int chp) {
-  return kHW2 + 256 * (bits_max + chp) <= kWAlloc;   // + the padding-row reads of ChEst
+// The truncated W2^T images put the LLR rows [0, bits_max) in the b2 slot of 16 outputs and
+// the ChEst rows [0, 2A) in a CHP-row slot: bits_max <= 16 and 2A <= CHP <= 32 are
+// required besides the byte budget (the padding rows the lanes read beyond the real ones
+// only reach output channels that are never stored).
+__host__ __device__ constexpr bool heads_fit_wb(int bits_max, int chp, int a2 = 0) {
+  return bits_max <= 16 && a2 <= chp && chp <= 32 && kHW2 + 256 * (bits_max + chp) <= kWAlloc;
 }
 
 template <class P, int CINP, int COUTP>
@@ -1626,6 +1630,11 @@ template <class P, int NW = 8>
 __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X, int b, int u, int f_start) {
   using S = typename P::S;
   static_assert(sizeof(S) == 2 && kUPD_CINP * 2 / 16 == 16, "f16 z image with 16 chunks per symbol row");
+  // the lane's symbol group is fixed at 4 (wave & 3) + tq and instruction k steps by NW: that
+  // matches k's symbol group 4 (k & 3) + tq only when NW is a multiple of 4 and the issuing
+  // waves w0 .. w0+NW-1 are 8-aligned as a set of residues mod 4
+  static_assert(NW % 4 == 0 && NW <= 8, "DMA-issuing wave count must be 4 or 8");
+  static_assert(NRX_DMA_HI == 0 || NW == 4, "NRX_DMA_HI needs NW == 4");
   constexpr int R0 = strip_slots<P>();
   constexpr int QS = kDS / P::EPC;   // 7 chunks of a, then 7 of s
   const auto& a = prm.a;
@@ -1987,13 +1996,18 @@ __global__ __launch_bounds__(512) void k_update(BlockParams<P> prm) {
 
 // ======================================================================= launchers
 
-// CUs per device, recorded by setup_kernels() (nrx_create) for the pairing heuristic;
-// 256 (MI355X) until then
+// CUs of the current device for the pairing / strip-tier heuristics, queried once per
+// device on first use (a single cached value was wrong for other devices)
 constexpr int kMaxDevices = 64;
 static int g_cu_count[kMaxDevices];
 static int cu_count() {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices || g_cu_count[dev] <= 0) return 256;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 256;
+  if (g_cu_count[dev] <= 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 256;
+    g_cu_count[dev] = cus;
+  }
   return g_cu_count[dev];
 }
 
@@ -2117,7 +2131,7 @@ struct Launch {
           const int items = (int)grid.x;
           pair_ro = NRX_PAIR != 0 && NRX_ZDMA != 0 && NRX_PAIR_RO != 0 && args.U <= 2 && bp.inline_combine &&
                     items % 16 == 0 && items >= 2 * cu_count() && args.H == 1 &&
-                    heads_fit_wb(args.bits_max, ch32 ? 32 : 16);
+                    heads_fit_wb(args.bits_max, ch32 ? 32 : 16, 2 * args.A);
           if (pair_ro) {
             constexpr int L_wb = strip_lds_bytes<P>(true);
             bp.pair = 1;
@@ -2179,11 +2193,7 @@ hipError_t launch_forward_f64(const FwdArgs<double, double, float>& args,
 }
 
 hipError_t setup_kernels() {
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) == hipSuccess &&
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0 &&
-      dev >= 0 && dev < kMaxDevices)
-    g_cu_count[dev] = cus;
+  (void)cu_count();
   hipError_t e = Launch<P16>::setup();
   hipError_t e1 = Launch<P16S>::setup();
   if (e1 == hipSuccess) e1 = Launch<P16M>::setup();

@@ -4,12 +4,15 @@ The counterpart of the reference's ``scripts/evaluate.py`` NRX leg (evaluate.py:
 ``E2E_Model`` + ``load_weights`` + ``num_it = num_nrx_iter_eval`` + Sionna ``sim_ber``),
 with the pieces that exist here: the GPU slot generator (``generator.SlotGenerator``),
 the CGNN engine, the GPU error counters, and -- across ranks -- one RCCL
-``all_reduce(SUM)`` of the int64 counters per Monte-Carlo iteration (the analogue of
-``sim_ber(distribute="all")``, evaluate.py:61).  Counts are uncoded (no LDPC here): BER
+``all_reduce(SUM)`` of the int64 counters every ``sync_every`` Monte-Carlo iterations
+(the analogue of ``sim_ber(distribute="all")``, evaluate.py:61).  Between those
+reductions nothing leaves the device: the counters accumulate in HBM and the host runs
+ahead, so a sharded run pays one collective + one host sync per window, not per batch.  Counts are uncoded (no LDPC here): BER
 of hard decisions on the LLRs and the fraction of (slot, user) grids with any bit error.
 
 sim_ber semantics kept: per Eb/N0 point iterate until ``max_mc_iter`` or until
-``num_target_block_errors`` block errors; ``early_stop`` ends the sweep at the first
+``num_target_block_errors`` block errors (tested at each reduction, so a point may run
+up to ``sync_every - 1`` batches past the target); ``early_stop`` ends the sweep at the first
 point without errors; ``target_bler`` ends it once the BLER falls below the target.
 
     python -m neural_rx_amd.evaluate -config_name nrx_rt -num_tx_eval 2 \
@@ -53,12 +56,17 @@ def _dist():
 def sim_ber(engine: CGNNEngine, gen: SlotGenerator, ebno_dbs: Sequence[float], batch_size: int,
             max_mc_iter: int = 100, num_target_block_errors: int = 100, target_bler: Optional[float] = None,
             early_stop: bool = True, num_it: Optional[int] = None, precision: str = "f16",
-            verbose: bool = False) -> SimResult:
+            verbose: bool = False, sync_every: int = 8) -> SimResult:
     """Sionna ``sim_ber`` loop on the GPU (this rank's shard of every Monte-Carlo batch:
-    global slot ``(it * world + rank) * batch_size + b``)."""
+    global slot ``(it * world + rank) * batch_size + b``).  The counters are reduced
+    over ranks (and copied to the host) every ``sync_every`` batches and at the end of a
+    point; every rank runs the same number of batches, so the collectives pair up."""
     import torch
     dist = _dist()
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
+    # gloo (CPU tests, or ranks sharing one device) reduces host tensors; nccl = RCCL
+    host_reduce = dist is not None and dist.get_backend() != "nccl"
+    sync_every = max(1, int(sync_every))
     p = gen.p
     dev = torch.device(f"cuda:{gen.device}")
     pe = torch.from_numpy(compute_pe(p.num_tx, p.num_subcarriers, p.dmrs_symbols, p.cdm_group)).to(dev)
@@ -80,7 +88,11 @@ def sim_ber(engine: CGNNEngine, gen: SlotGenerator, ebno_dbs: Sequence[float], b
                                     precision=precision, out=llr_out, want_h=False)
             count_errors(llr, sb.bits, sb.active, sb.mcs, p.mcs_bits, p.dmrs_symbols, counts=counts)
             it += 1
+            if it % sync_every and it < max_mc_iter:
+                continue
             tot = counts.sum(0)
+            if host_reduce:
+                tot = tot.cpu()
             if dist:
                 dist.all_reduce(tot)
             total = tot.cpu().numpy()
@@ -120,6 +132,7 @@ def main(argv=None):
     ap.add_argument("-var_mcs", action="store_true", help="draw the MCS of every (slot, user)")
     ap.add_argument("-precision", default="f16")
     ap.add_argument("-seed", type=int, default=1234)
+    ap.add_argument("-sync_every", type=int, default=8, help="MC batches per counter all-reduce")
     ap.add_argument("-gpu", type=int, default=None)
     ap.add_argument("-out", default=None, help="write the result JSON here")
     a = ap.parse_args(argv)
@@ -143,7 +156,7 @@ def main(argv=None):
     gen = SlotGenerator(params, device=device)
     ebno = a.ebno_db if a.ebno_db is not None else list(np.arange(-2.0, 8.0, 1.0))
     res = sim_ber(engine, gen, ebno, a.batch_size, a.max_mc_iter, a.num_target_block_errors, a.target_bler,
-                  num_it=cfg.num_nrx_iter_eval, precision=a.precision, verbose=True)
+                  num_it=cfg.num_nrx_iter_eval, precision=a.precision, verbose=True, sync_every=a.sync_every)
     if rank == 0:
         d = res.as_dict()
         d.update(config=cfg.label, num_tx_eval=params.num_active, dmrs_symbols=list(dmrs_symbols(cfg)),

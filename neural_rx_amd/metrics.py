@@ -62,6 +62,27 @@ def io_bytes_per_slot(spec: ModelSpec, num_tx: int, num_subcarriers: int, elem: 
     return {"in": inp, "out": out}
 
 
+def update_launch_split_per_re_user(spec: ModelSpec, num_it: int) -> dict:
+    """The k_update launch's algorithmic FLOPs split by the pipe that executes them:
+    the depthwise 3x3 taps run on the VALU (packed f16 FMAs), everything else (pointwise
+    1x1 and the dense MLPs of the fused tails) on the MFMA pipe."""
+    v1, v2 = spec.state_units
+    dw = 2 * 9 * (spec.update_in_ch + v1 + v2)
+    total = launch_flops_per_re_user(spec, num_it)["state_update"]
+    return {"depthwise_valu": dw, "dense_mfma": total - dw, "total": total}
+
+
+def mixed_bound_tflops(spec: ModelSpec, num_it: int, mfma_tflops: float = 2500.0,
+                       valu_tflops: float = 157.3) -> float:
+    """Roofline of the k_update launch when each FLOP runs on its own pipe at that pipe's
+    peak and the two pipes overlap perfectly: total / (dense / MFMA peak + depthwise /
+    VALU peak).  The VALU peak is the f32 vector peak; packed f16 FMAs issue at the same
+    wave-instruction rate on gfx950 (tools/ubench/valu_occ.hip)."""
+    s = update_launch_split_per_re_user(spec, num_it)
+    return s["total"] / (s["dense_mfma"] / mfma_tflops + s["depthwise_valu"] / valu_tflops)
+
+
 # MI355X peaks (MI355X_MICROARCH.md "Chip-level parameters")
 PEAK_TFLOPS = {"f16": 2500.0, "f32x": 78.6}   # dense f16 MFMA; f64 MFMA (spec, = FP32/2)
 PEAK_HBM_GBS = 8000.0
+PEAK_VALU_TFLOPS = 157.3                       # f32 vector peak (= packed f16 issue rate)

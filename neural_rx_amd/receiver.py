@@ -105,11 +105,11 @@ class CGNNEngine:
         return float(self._lib.nrx_flops_per_re_user(ctypes.byref(self._desc),
                                                      num_it or self.spec.num_it))
 
-    def workspace_bytes(self, batch, num_tx, num_subcarriers, precision="f16") -> int:
+    def workspace_bytes(self, batch, num_tx, num_subcarriers, precision="f16", y_layout="cgnn") -> int:
         shape = _lib.nrx_shape(batch, num_tx, num_subcarriers, NUM_SYMBOLS)
         out = ctypes.c_size_t()
-        _lib.check(self._lib.nrx_workspace_size(self._h, ctypes.byref(shape),
-                                                _lib.PRECISIONS[precision], ctypes.byref(out)))
+        _lib.check(self._lib.nrx_workspace_size_ex(self._h, ctypes.byref(shape), _lib.PRECISIONS[precision],
+                                                   _lib.Y_LAYOUTS[y_layout], ctypes.byref(out)))
         return out.value
 
     def _workspace(self, nbytes: int):
@@ -132,34 +132,55 @@ class CGNNEngine:
 
     # -------------------------------------------------------------- forward
     def forward(self, y, pe, h_hat, active, mcs_mask=None, num_it=None, precision="f16",
-                out=None, want_h=True, stream=None):
-        """All inputs are float32 CUDA tensors in the CGNN layout (see include/nrx.h).
-        Returns ``(llr [H,B,U,F,T,bits_max], h_ref [B,U,F,T,2A] or None)``."""
+                out=None, want_h=True, stream=None, y_layout="cgnn", y_imag=None):
+        """All inputs are float32 CUDA tensors in the CGNN layout (see include/nrx.h), except
+        ``y`` with ``y_layout``: "sionna" = the complex64 resource grid ``[B,1,A,14,F]``
+        CGNNOFDM.forward receives, "split" = ``y`` / ``y_imag`` = rx_slot_real / imag
+        ``[B,F,14,A]`` (NeuralReceiverONNX); the layout change runs in libnrx
+        (``nrx_forward_ex``).  Returns ``(llr [H,B,U,F,T,bits_max], h_ref [B,U,F,T,2A] or
+        None)``."""
         torch = _torch()
         sp = self.spec
-        if y.dim() != 4 or y.shape[2] != NUM_SYMBOLS or y.shape[3] != 2 * sp.num_rx_ant:
-            raise ValueError(f"y must be [B,F,14,{2 * sp.num_rx_ant}], got {tuple(y.shape)}")
-        B, F = y.shape[0], y.shape[1]
+        A = sp.num_rx_ant
+        if y_layout == "cgnn":
+            if y.dim() != 4 or y.shape[2] != NUM_SYMBOLS or y.shape[3] != 2 * A:
+                raise ValueError(f"y must be [B,F,14,{2 * A}], got {tuple(y.shape)}")
+            B, F = y.shape[0], y.shape[1]
+        elif y_layout == "sionna":
+            if y.is_complex():
+                if y.dtype != torch.complex64:
+                    raise ValueError("the resource grid must be complex64")
+                y = torch.view_as_real(y.contiguous())
+            if y.dim() != 6 or y.shape[1] != 1 or y.shape[2] != A or y.shape[3] != NUM_SYMBOLS or y.shape[5] != 2:
+                raise ValueError(f"resource grid must be [B,1,{A},14,F] complex, got {tuple(y.shape)}")
+            B, F = y.shape[0], y.shape[4]
+        elif y_layout == "split":
+            if y.dim() != 4 or y.shape[2] != NUM_SYMBOLS or y.shape[3] != A or y_imag is None or \
+                    tuple(y_imag.shape) != tuple(y.shape):
+                raise ValueError(f"rx_slot_real / rx_slot_imag must be [B,F,14,{A}]")
+            B, F = y.shape[0], y.shape[1]
+        else:
+            raise ValueError(f"unknown y layout {y_layout}")
         U = active.shape[1]
         if tuple(pe.shape) != (U, F, NUM_SYMBOLS, 2):
             if pe.shape[0] >= U and tuple(pe.shape[1:]) == (F, NUM_SYMBOLS, 2):
                 pe = pe[:U]          # pe[:num_tx] (neural_rx.py:817)
             else:
                 raise ValueError(f"pe must be [U,F,14,2], got {tuple(pe.shape)}")
-        if h_hat is not None and tuple(h_hat.shape) != (B, U, F, NUM_SYMBOLS, 2 * sp.num_rx_ant):
+        if h_hat is not None and tuple(h_hat.shape) != (B, U, F, NUM_SYMBOLS, 2 * A):
             raise ValueError(f"h_hat has shape {tuple(h_hat.shape)}")
         if mcs_mask is not None and tuple(mcs_mask.shape) != (B, U, sp.num_mcs):
             mcs_mask = mcs_mask.expand(B, U, sp.num_mcs)
-        tensors = [y, pe, h_hat, active, mcs_mask]
+        tensors = [y, pe, h_hat, active, mcs_mask, y_imag if y_layout == "split" else None]
         for t in tensors:
             if t is not None and (not t.is_cuda or t.dtype != torch.float32):
                 raise ValueError("inputs must be float32 CUDA tensors")
-        y, pe, h_hat, active, mcs_mask = [None if t is None else t.contiguous() for t in tensors]
+        y, pe, h_hat, active, mcs_mask, y_im = [None if t is None else t.contiguous() for t in tensors]
         if out is None:
             out = self.alloc_outputs(B, U, F, want_h)
         llr, h_ref = out
         prec = _lib.PRECISIONS[precision]
-        nbytes = self.workspace_bytes(B, U, F, precision)
+        nbytes = self.workspace_bytes(B, U, F, precision, y_layout)
         ws = self._workspace(nbytes)
         io = _lib.nrx_io()
         io.shape = _lib.nrx_shape(B, U, F, NUM_SYMBOLS)
@@ -171,11 +192,12 @@ class CGNNEngine:
         io.h_ref = h_ref.data_ptr() if h_ref is not None else None
         if stream is None:
             stream = torch.cuda.current_stream(y.device).cuda_stream
-        _lib.check(self._lib.nrx_forward(self._h, ctypes.byref(io), ws.data_ptr(), ws.numel(), stream))
+        _lib.check(self._lib.nrx_forward_ex(self._h, ctypes.byref(io), _lib.Y_LAYOUTS[y_layout],
+                                            y_im.data_ptr() if y_im is not None else None, ws.data_ptr(),
+                                            ws.numel(), stream))
         # keep inputs alive until the stream consumed them
         self._last_inputs = tensors
         return llr, h_ref
-
 
     # -------------------------------------------------------------- coded-bit layout
     def llr_demap(self, llr_head, bits, data_re, stream=None):
@@ -310,12 +332,12 @@ class CGNN:
         assert (val >= 1) and (val <= self.spec.num_it), "Invalid number of iterations"
         self._num_it = val
 
-    def forward(self, inputs):
+    def forward(self, inputs, y_layout="cgnn", y_imag=None):
         """``inputs = [y, pe, h_hat, active_tx, mcs_ue_mask]`` -> ``(llrs, h_hats)`` with
         ``llrs[-1][m]`` = LLRs of MCS m ``[B,U,F,T,bits_m]`` and ``h_hats[-1]``."""
         y, pe, h_hat, active_tx, mcs_ue_mask = inputs
         llr, h = self.engine.forward(y, pe, h_hat, active_tx, mcs_ue_mask, self._num_it,
-                                     self.precision)
+                                     self.precision, y_layout=y_layout, y_imag=y_imag)
         self.last_raw_llr = llr          # [H, B, U, F, T, bits_max] (for coded-bit demapping)
         sp = self.spec
         per_mcs = []
@@ -333,7 +355,13 @@ class NeuralReceiver:
     def __init__(self, config: str | NRXConfig = "nrx_rt", weight_list=None, device: int = 0,
                  precision: str = "f16", num_rx_ant: Optional[int] = None,
                  cdm_groups: Optional[Sequence[int]] = None):
-        self.cgnn = CGNN(config, weight_list, device, precision, num_rx_ant)
+        cfg = get_config(config) if isinstance(config, str) else config
+        if cfg.mask_pilots:
+            # CGNNOFDM.forward zeroes y on the pilot REs of the resource-grid type grid when
+            # mask_pilots is set (neural_rx.py:828-830).  Only the e2e configs set it, and
+            # their models (learned constellation, no h_hat, d_s = 64) are out of scope.
+            raise NotImplementedError("mask_pilots = True (e2e configs) is not supported by this engine")
+        self.cgnn = CGNN(cfg, weight_list, device, precision, num_rx_ant)
         self.cfg = self.cgnn.cfg
         self.spec = self.cgnn.spec
         self.device = device
@@ -366,39 +394,80 @@ class NeuralReceiver:
                 f"cuda:{self.device}")
         return self._pe_cache[key]
 
+    def _mcs_mask(self, mcs_arr_eval, B, U, device):
+        """CGNNOFDM.forward's default mask: one_hot(mcs_arr_eval[0]) (neural_rx.py:817-820)."""
+        torch = _torch()
+        m = torch.zeros((B, U, self.spec.num_mcs), dtype=torch.float32, device=device)
+        m[..., int(mcs_arr_eval[0])] = 1.0
+        return m
+
     def __call__(self, rx_grid, pe=None, active_dmrs=None, h_hat=None, mcs_ue_mask=None,
-                 num_it=None, layout: str = "sionna", return_h_hat: bool = False, demap: bool = False):
+                 num_it=None, layout: str = "sionna", return_h_hat: bool = False, demap: bool = False,
+                 mcs_arr_eval: Optional[Sequence[int]] = None, all_mcs: bool = False):
+        """``layout`` "sionna": rx_grid = y ``[B,1,A,14,F]`` complex (CGNNOFDM.forward);
+        "aerial": rx_grid = (rx_slot_real, rx_slot_imag) ``[B,F,14,A]`` and LLRs returned as
+        ``[B,bits,U,F,T]`` with the Aerial sign (NeuralReceiverONNX.forward); "cgnn": rx_grid
+        is already ``[B,F,14,2A]``.
+
+        ``mcs_arr_eval`` (CGNNOFDM.forward(inputs, mcs_arr_eval, mcs_ue_mask_eval)): the MCS
+        indices to read out; without ``mcs_ue_mask`` the state-init mask is
+        one_hot(mcs_arr_eval[0]).  With ``demap`` the output is the coded bits of the data
+        REs ``[B,U,num_coded_bits]`` of head mcs_arr_eval[0] (the reference returns
+        ``llrs[-1][0]``, neural_rx.py:881); ``all_mcs`` returns the list for every listed
+        MCS, each demapped with its own head and bit count (neural_rx.py:843-852)."""
         torch = _torch()
         if num_it is not None:
             self.num_it = num_it
+        y_imag = None
         if layout == "sionna":
-            # CGNNOFDM.forward: y [B,1,A,T,F] complex -> [B,F,T,2A] (neural_rx.py:831-833)
-            y = rx_grid[:, 0].permute(0, 3, 2, 1)
-            y = torch.cat([y.real, y.imag], dim=-1).to(torch.float32).contiguous()
+            # CGNNOFDM.forward: y [B,1,A,T,F] complex -> [B,F,T,2A] (neural_rx.py:831-833),
+            # done by libnrx (nrx_forward_ex, NRX_Y_SIONNA_RG)
+            y, y_layout = rx_grid, "sionna"
+            if not y.is_complex():
+                y = y.to(torch.complex64)
+            B, F = y.shape[0], y.shape[4]
         elif layout == "aerial":
             # NeuralReceiverONNX.forward: (rx_slot_real, rx_slot_imag) [B,F,T,A]
-            y_re, y_im = rx_grid
-            y = torch.cat([y_re, y_im], dim=-1).to(torch.float32).contiguous()
+            y, y_imag = rx_grid
+            y, y_imag, y_layout = y.to(torch.float32), y_imag.to(torch.float32), "split"
+            B, F = y.shape[0], y.shape[1]
         elif layout == "cgnn":
-            y = rx_grid
+            y, y_layout = rx_grid, "cgnn"
+            B, F = y.shape[0], y.shape[1]
         else:
             raise ValueError(f"unknown layout {layout}")
-        B, F = y.shape[0], y.shape[1]
+        dev = y.device
         if active_dmrs is None:
-            active_dmrs = torch.ones((B, self.cfg.max_num_tx), dtype=torch.float32, device=y.device)
+            active_dmrs = torch.ones((B, self.cfg.max_num_tx), dtype=torch.float32, device=dev)
         active = active_dmrs.to(torch.float32).contiguous()
         U = active.shape[1]
         if pe is None:
             pe = self.positional_encoding(U, F)
-        llrs, h_hats = self.cgnn([y, pe, h_hat, active, mcs_ue_mask])
+        if mcs_arr_eval is None:
+            mcs_arr_eval = [0]
+        for m in mcs_arr_eval:
+            if not 0 <= int(m) < self.spec.num_mcs:
+                raise ValueError(f"mcs index {m} outside 0..{self.spec.num_mcs - 1}")
+        if mcs_ue_mask is None and self.spec.num_mcs > 1:
+            mcs_ue_mask = self._mcs_mask(mcs_arr_eval, B, U, dev)
+        llrs, h_hats = self.cgnn([y, pe, h_hat, active, mcs_ue_mask], y_layout=y_layout, y_imag=y_imag)
         h_ref = h_hats[-1]
         if demap:
             # CGNNOFDM.forward's output (neural_rx.py:843-858): per-user coded bits of the
-            # data REs, [B, U, num_coded_bits] for MCS 0 (mcs_arr_eval[0])
+            # data REs, [B, U, num_coded_bits], one entry per listed MCS with its own head
             raw = self.cgnn.last_raw_llr
-            llr = self.cgnn.engine.llr_demap(raw[0], self.spec.bits[0], self.data_re(F))
+            sp = self.spec
+            outs = []
+            for m in (mcs_arr_eval if all_mcs else mcs_arr_eval[:1]):
+                head = 0 if sp.masking else int(m)
+                outs.append(self.cgnn.engine.llr_demap(raw[head], sp.bits[int(m)], self.data_re(F)))
+            llr = outs if all_mcs else outs[0]
             return (llr, h_ref) if return_h_hat else llr
-        llr = llrs[-1][0] if self.spec.num_mcs == 1 else llrs[-1]
+        if all_mcs:
+            llr = [llrs[-1][int(m)] for m in mcs_arr_eval]
+        else:
+            llr = llrs[-1][int(mcs_arr_eval[0])] if self.spec.num_mcs > 1 else llrs[-1][0]
         if layout == "aerial":
-            llr = -llr.permute(0, 4, 1, 2, 3)   # [B,bits,U,F,T], LLR = log p0/p1
+            neg = lambda t: -t.permute(0, 4, 1, 2, 3)   # [B,bits,U,F,T], LLR = log p0/p1
+            llr = [neg(t) for t in llr] if all_mcs else neg(llr)
         return (llr, h_ref) if return_h_hat else llr

@@ -35,3 +35,16 @@ def test_mcs_bits_and_specs():
     assert sp.masking and sp.head_bits == [6] and sp.num_init == 1
     sp = spec_from_config(BUILTIN["nrx_rt_var_mcs"])
     assert sp.num_init == 2 and sp.head_bits == [2, 4]
+
+
+def test_mask_pilots_rejected():
+    # CGNNOFDM.forward zeroes the pilot REs of y when mask_pilots is set (neural_rx.py:828-830);
+    # only the e2e configs set it and they are out of scope: the wrapper refuses them before
+    # creating an engine (no GPU needed for this check)
+    import dataclasses
+    import pytest
+    from neural_rx_amd.config import get_config
+    from neural_rx_amd.receiver import NeuralReceiver
+    cfg = dataclasses.replace(get_config("nrx_rt"), mask_pilots=True)
+    with pytest.raises(NotImplementedError, match="mask_pilots"):
+        NeuralReceiver(cfg)

@@ -1,0 +1,96 @@
+"""Oracle parity at the BASELINE.json launch shapes (needs an MI355X).
+
+Every configuration of BASELINE.json runs here at the size the bench runs it per GPU (the
+8-GPU configs at their per-GPU shard; cfg3 / cfg5 as one full-width slot, the oracle's
+budget), and the HIP output is compared with the fp64 numpy oracle
+(``oracle/cgnn_ref.cgnn_forward``, semantics neural_rx.py:544-595).  So the launch paths
+the bench takes -- paired aggregation-tail items, paired readout items with the heads in
+WB, Var-IO heads, the k_norm pass and the k_combine pass for U > 4 -- are checked
+against the oracle directly, not only for self-consistency.
+
+Tolerances are the ones of tests/test_gpu_parity.py:
+* f32x (f32 storage, f64 arithmetic): LLR max-abs < 1e-3, h_hat max-abs < 1e-4.
+* f16: max-abs <= 10 % of max|LLR|, RMS <= 2 % of RMS(LLR), hard-decision flips
+  <= 0.5 % overall and <= 0.1 % where |LLR| > 0.5.
+"""
+import numpy as np
+import pytest
+
+from tests.helpers import compare, make_case, run_engine, run_oracle
+from tests.test_gpu_parity import (F16_FLIP_CONF_TOL, F16_FLIP_TOL, F16_REL_TOL, F16_RMS_TOL, F32X_H_TOL,
+                                   F32X_LLR_TOL, engine_for)
+
+pytestmark = pytest.mark.gpu
+
+
+def check(case, f32x=True):
+    ref = run_oracle(case)
+    out = {}
+    if f32x:
+        got = run_engine(case, "f32x", engine_for(case))
+        c = compare(ref, got)
+        assert np.isfinite(got["llr_raw"]).all()
+        assert c["llr_maxabs"] < F32X_LLR_TOL, c
+        assert c["h_maxabs"] < F32X_H_TOL, c
+        out["f32x"] = c
+    got16 = run_engine(case, "f16", engine_for(case))
+    c16 = compare(ref, got16)
+    assert np.isfinite(got16["llr_raw"]).all()
+    assert c16["llr_rel"] <= F16_REL_TOL, c16
+    assert c16["llr_rms_rel"] <= F16_RMS_TOL, c16
+    assert c16["flip_rate"] <= F16_FLIP_TOL, c16
+    assert c16["flip_rate_confident"] <= F16_FLIP_CONF_TOL, c16
+    out["f16"] = c16
+    print({k: {m: round(v, 6) for m, v in d.items()} for k, d in out.items()})
+    return out
+
+
+def test_cfg1_nrx_rt_1ue_b1():
+    # BASELINE configs[0]: nrx_rt, 1 UE, 4 PRB, 4 rx ant, 16-QAM, batch 1 (latency tier:
+    # 8-row strips, unpaired launches)
+    check(make_case("nrx_rt", batch=1, users=1, prbs=4, snr_db=15, seed=21))
+
+
+def test_cfg2_nrx_rt_2ue_b128():
+    # BASELINE configs[1], the bench workload: B = 128, U = 2 -> 512 items, so both update
+    # launches run paired (aggregation tail; readout tail with the heads in WB)
+    check(make_case("nrx_rt", batch=128, users=2, prbs=4, snr_db=12, seed=22))
+
+
+def test_cfg2_random_activity_b128():
+    # the bench shape with inactive users (act = 0 rows, p = 1 / (#active - 1))
+    rng = np.random.default_rng(23)
+    active = (rng.random((128, 2)) < 0.7).astype(np.float32)
+    check(make_case("nrx_rt", batch=128, users=2, prbs=4, snr_db=12, seed=23, active=active))
+
+
+def test_cfg4_var_io_random_mcs_b128():
+    # BASELINE configs[3] per-GPU shard (1024 / 8): Var-IO with a random one-hot MCS per
+    # (slot, user) over {QPSK, 16-QAM}: two StateInit launches, two LLR heads
+    rng = np.random.default_rng(24)
+    mcs = rng.integers(0, 2, size=(128, 2))
+    check(make_case("nrx_rt_var_mcs", batch=128, users=2, prbs=4, snr_db=12, seed=24, mcs_choice=mcs))
+
+
+def test_cfg4b_masking_64qam_b32():
+    # BASELINE configs[3] 64-QAM variant (cfg 4'): masking model, 8 iterations,
+    # one 6-bit head sliced per MCS; random MCS in {QPSK, 16-QAM, 64-QAM}
+    rng = np.random.default_rng(25)
+    mcs = rng.integers(0, 3, size=(32, 2))
+    check(make_case("nrx_large_var_mcs_64qam_masking", batch=32, users=2, prbs=4, snr_db=22, seed=25,
+                    mcs_choice=mcs))
+
+
+def test_cfg3_full_slot_132prb_16ant_4ue():
+    # BASELINE configs[2] topology at full width: 132 PRB (F = 1584), 16 rx antennas
+    # (StateInit in-ch 66, ChEst out 32), 4 users, nrx_large (8 iterations); seeded weights
+    # (no trained 16-antenna model exists), one slot; the k_norm pass runs (large grid)
+    case = make_case("nrx_large", batch=1, users=4, prbs=132, num_rx_ant=16, seeded_weights=True,
+                     random_inputs=True, seed=26)
+    check(case)
+
+
+def test_cfg5_full_slot_273prb_8ue_64qam():
+    # BASELINE configs[4] at full width: 273 PRB (F = 3276), 8 users (U > 4: k_combine),
+    # 64-QAM, nrx_large_64qam (8 iterations), one slot
+    check(make_case("nrx_large_64qam", batch=1, users=8, prbs=273, snr_db=25, seed=27))

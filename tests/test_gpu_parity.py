@@ -145,9 +145,11 @@ def test_receiver_layouts_consistent():
 
 # Paired update path (two aggregation-tail items per workgroup, the second item's z image
 # DMA'd during the first one's epilogue; taken when items % 16 == 0 and items >= 2 x CUs).
-# Each case is compared bit for bit with an unpaired run of a few of its slots (small B: one
-# item per workgroup): a slot's outputs must not depend on the batch it runs in or on which
-# workgroup ran it.  Cases: the bench shape; U = 1 (no other user: zero aggregate chunks);
+# Each case is compared bit for bit with a run of only 4 of its slots: a slot's outputs must
+# not depend on the batch it runs in or on which workgroup ran it.  The 4-slot run has no
+# more items than CUs, so it takes the small-strip tier (8-row strips, P16S, unpaired): the
+# check covers pairing AND strip-width invariance together (a failure does not say which;
+# tests/test_gpu_baseline_shapes.py compares the paired bench path with the oracle directly).  Cases: the bench shape; U = 1 (no other user: zero aggregate chunks);
 # a random active mask (act = 0 users, p = 1 / (#active - 1)); B = 136 (not a multiple of 8:
 # work_item's plain-order tail); F = 60 (a partial last strip, 3 strips).  The last update
 # pairs too when its heads fit beside the strip image (TAIL_READOUT_WB: one LLR head, W2

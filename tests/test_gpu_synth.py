@@ -168,6 +168,9 @@ def test_sim_ber_loop():
     assert r.counts[0][3] == 4 * 32 * 2
     assert r.ber[0] > r.ber[1] > r.ber[2]
     assert r.ber[2] < 1e-2 and r.ber[0] > 5e-2
-    # target block errors stop a point early
-    r2 = sim_ber(eng, gen, [0.0], batch_size=32, max_mc_iter=50, num_target_block_errors=1)
+    # target block errors stop a point early -- tested at each counter reduction, i.e. every
+    # sync_every batches (one host sync / all-reduce per window)
+    r2 = sim_ber(eng, gen, [0.0], batch_size=32, max_mc_iter=50, num_target_block_errors=1, sync_every=1)
     assert r2.mc_iters == [1]
+    r3 = sim_ber(eng, gen, [0.0], batch_size=32, max_mc_iter=50, num_target_block_errors=1, sync_every=8)
+    assert r3.mc_iters == [8]

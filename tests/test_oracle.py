@@ -154,3 +154,23 @@ def test_fp32_oracle_close_to_fp64():
     r32 = run_oracle(case, dtype=np.float32)
     d = np.abs(r64["llr"][0] - r32["llr"][0]).max()
     assert d < 1e-2
+
+
+@pytest.mark.parametrize("config,users,kw", [
+    ("nrx_rt", 2, {}),
+    ("nrx_rt_var_mcs", 2, {"mcs_choice": [[0, 1], [1, 0]]}),
+    ("nrx_large_var_mcs_64qam_masking", 2, {"mcs_choice": [[2, 0], [1, 2]], "snr_db": 22}),
+])
+def test_torch_cpu_restatement_matches_numpy_oracle(config, users, kw):
+    # oracle/cgnn_torch.py (conv2d(groups=C) + 1x1 conv, the CPU baseline) vs the numpy
+    # oracle: two independent restatements of the same TF model agree to fp32 rounding
+    from oracle import cgnn_ref
+    from oracle.cgnn_torch import TorchCGNN
+    case = make_case(config, batch=2, users=users, prbs=2, **kw)
+    w = cgnn_ref.split_keras_weights(case.weights, case.spec)
+    ref = run_oracle(case)
+    got = TorchCGNN(w, case.spec).forward(case.y, case.pe, case.h_hat, case.active, case.mcs_mask)
+    for r, g in zip(ref["llr"], got["llr"]):
+        assert r.shape == g.shape
+        assert np.abs(r - g).max() < 2e-3
+    assert np.abs(ref["h_hat"] - got["h_hat"]).max() < 1e-4
