@@ -30,6 +30,47 @@ constexpr int kMaxHeads = 8;
 constexpr int kMaxUsers = 16;
 constexpr int kHalo = 3;      // 3 stacked 3x3 convs per block
 
+// ---- LDS images of the f16 weights (kernels: SepStage / DenseStage / nrx_rr.inc DMA;
+// host: nrx_api.cpp packs the same bytes for LDS-DMA).  A W^T [COUTP][CINP] image is a stack
+// of 16-row tiles addressed like an activation image: element (co, chunk q of 8 inputs) at
+// lds_off<NQ>(co >> 4, co & 15, q), NQ = CINP / 8 chunks per row, chunk index XOR-swizzled
+// with the row so that a ds_read_b128 lane group hits distinct bank slots.
+constexpr int kTPImg = 16;
+__host__ __device__ constexpr int swz_q(int nq, int t) {
+  return nq >= 16 ? (t & 15) : (nq == 8 ? ((t >> 1) & 7) : (nq == 4 ? ((t >> 2) & 3) : 0));
+}
+__host__ __device__ constexpr int lds_img_off(int nq, int row, int t, int q) {
+  return ((row * kTPImg + t) * nq + (q ^ swz_q(nq, t))) * 16;
+}
+// separable layer: pw^T at 0 (<= 32 KB), dw [9][CINP] at kWPw, bias [COUTP] f32 at kWBias
+constexpr int kWPw = kHID * kHID * 2;          // 32 KB
+constexpr int kWDw = 9 * kHID * 2;             // 2304 B
+constexpr int kWBias = kWPw + kWDw;            // conv bias [COUTP] f32
+constexpr int kWTailBias = kWBias + kHID * 4;  // aggregation-MLP biases (2 x 64 f32)
+constexpr int kWBytes = kWTailBias + 2 * kAGG * 4;
+// readout heads (TAIL_READOUT_WB layout): LLR W1^T at 0, ChEst W1^T at kHW1C, biases, then
+// the W2^T images truncated to their real rows
+constexpr int kHW1C = 16 * 1024;                 // ChEst W1^T (LLR W1^T at 0)
+constexpr int kHB1 = 32 * 1024;                  // b1: LLR [128] f32, ChEst [128] f32
+constexpr int kHB2 = kHB1 + 2 * kHID * 4;        // b2: LLR [16] f32, ChEst [<= 32] f32
+constexpr int kHW2 = kHB2 + (16 + 32) * 4;       // LLR W2^T rows [bits], then ChEst rows [2A]
+// register-resident blocks (nrx_rr.inc): a sep image without the tail biases, the
+// aggregation-MLP tail image (W1^T 64x64 | W2^T 64x64 | b1 | b2), the heads image budget
+constexpr int kRrABytes = kWPw + kWDw + kHID * 4;   // 35 584
+constexpr int kRrBBytes = 37632;
+constexpr int kRrTailB = kWTailBias - 16 * 1024;    // 18 944
+constexpr int kRrTailBytes = kRrTailB + 2 * kAGG * 4;
+__host__ __device__ constexpr int rr_heads_bytes(int bits_max, int a2) { return kHW2 + 256 * (bits_max + a2); }
+
+// Device copies of the LDS images (f16 model; null where a layer has none).
+struct RrImages {
+  const char* init[kMaxInit][3];
+  const char* upd[kMaxIt][3];
+  const char* tail[kMaxIt];     // aggregation MLP of iteration i
+  const char* heads;            // LLR head 0 + ChEst (one LLR head only), or null
+  int heads_bytes;
+};
+
 template <class WT, class BT>
 struct SepW {
   const WT* dw;

@@ -100,6 +100,40 @@ __device__ __forceinline__ void fmac_shr(half2& d, half2 x, half2 w) {
 __device__ __forceinline__ void fmac_shl(half2& d, half2 x, half2 w) {
   asm("v_pk_fmac_f16_dpp %0, %1, %2 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(d) : "v"(x), "v"(w));
 }
+// y * ns rounded to f32 before the storage conversion: without the barrier the compiler fuses
+// the product and the f16 conversion into one single-rounding v_fma_mix in some kernels and
+// not in others (1-ulp z differences between kernel families)
+__device__ __forceinline__ float f32_rounded(float v) {
+  asm("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ double f32_rounded(double v) { return v; }
+
+// The depthwise results are written by inline-asm DPP FMAs, whose latency the compiler's
+// hazard recognizer does not model: an MFMA that reads one as its B operand right behind
+// the last FMA can read the register before the write lands (seen as a wrong first output
+// tile of the last row of a 2-row pass).  This fence sits between the depthwise of a K
+// chunk and its MFMAs (the d values flow through it) and pads the VALU -> MFMA-operand
+// wait states.
+template <int R>
+__device__ __forceinline__ void dw_mfma_fence(half8 (&d)[R]) {
+  if constexpr (R == 1) asm volatile("s_nop 3" : "+v"(d[0]));
+  else if constexpr (R == 2) asm volatile("s_nop 3" : "+v"(d[0]), "+v"(d[1]));
+  else if constexpr (R == 3) asm volatile("s_nop 3" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]));
+  else asm volatile("s_nop 3" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]));
+}
+template <int R>
+__device__ __forceinline__ void dw_mfma_fence(doublex4 (&)[R]) {}
+// Same for the depthwise's DPP source rows when they are VALU results (z rows converted in
+// registers, the previous layer's outputs): a VALU write needs two wait states before a DPP
+// reads the register, which the compiler does not insert in front of inline asm.
+template <int N>
+__device__ __forceinline__ void dw_src_fence(half8 (&x)[N]) {
+  if constexpr (N == 3) asm volatile("s_nop 1" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]));
+  else if constexpr (N == 4) asm volatile("s_nop 1" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]));
+  else asm volatile("s_nop 1" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]));
+}
+
 __device__ __forceinline__ half2 h2(half8 v, int k) {
   return half2{v[2 * k], v[2 * k + 1]};
 }
@@ -139,7 +173,10 @@ struct P16T {
   // depthwise 3x3 of one output row from its three input rows (x0 = f-1, x1 = f, x2 = f+1);
   // tap = i*3 + j, i along subcarriers, j along symbols (j = 0 reads t-1).
   __device__ static DV dw_row(DV x0, DV x1, DV x2, const DV (&w)[9]) {
-    const DV c = w[1] * x0 + w[4] * x1 + w[7] * x2;
+    // the centre column's contraction is fixed in the source (not left to the compiler,
+    // which contracted it differently in different kernels: 1-ulp differences between
+    // strip widths / kernel families)
+    const DV c = __builtin_elementwise_fma(w[7], x2, __builtin_elementwise_fma(w[4], x1, w[1] * x0));
     half2 d[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -264,13 +301,8 @@ __device__ __forceinline__ int xoff(int slot, int t, int q) {
   return slot * slot_pitch<P>() + (t * NQ + (q ^ swz<NQ>(t))) * 16;
 }
 
-// Per-layer weight image in LDS (P16): W^T [COUTP][CINP] as 16-row tiles addressed like an
-// activation image (co>>4, co&15, chunk), then dw [9][CINP], then bias [COUTP] (f32).
-constexpr int kWPw = kHID * kHID * 2;          // 32 KB
-constexpr int kWDw = 9 * kHID * 2;             // 2304 B
-constexpr int kWBias = kWPw + kWDw;            // conv bias [COUTP] f32
-constexpr int kWTailBias = kWBias + kHID * 4;  // aggregation-MLP biases (2 x 64 f32)
-constexpr int kWBytes = kWTailBias + 2 * kAGG * 4;
+// Per-layer weight image in LDS (P16): layout constants kWPw .. kHW2 in nrx_internal.h
+// (shared with the host, which packs the same images for the LDS-DMA of nrx_rr.inc).
 // The paired readout tail gives WB the rest of the 160 KB LDS (P16: 160 KB - 30 x 4 KB) and
 // stages the heads there, so that the strip image X is free for the next item's z DMA
 // during the readout epilogue.  W1^T images in full; W2^T images truncated to their real
@@ -278,10 +310,6 @@ constexpr int kWBytes = kWTailBias + 2 * kAGG * 4;
 // output channels that are never stored.  One LLR head only.
 constexpr int kWAlloc = 160 * 1024 - 30 * kTP * kHID * 2;
 static_assert(kWBytes <= kWAlloc, "layer weight image exceeds the LDS left by the strip image");
-constexpr int kHW1C = 16 * 1024;                 // ChEst W1^T (LLR W1^T at 0)
-constexpr int kHB1 = 32 * 1024;                  // b1: LLR [128] f32, ChEst [128] f32
-constexpr int kHB2 = kHB1 + 2 * kHID * 4;        // b2: LLR [16] f32, ChEst [<= 32] f32
-constexpr int kHW2 = kHB2 + (16 + 32) * 4;       // LLR W2^T rows [bits], then ChEst rows [2A]
 // The truncated W2^T images put the LLR rows [0, bits_max) in the b2 slot of 16 outputs and
 // the ChEst rows [0, 2A) in a CHP-row slot: bits_max <= 16 and 2A <= CHP <= 32 are
 // required besides the byte budget (the padding rows the lanes read beyond the real ones
@@ -483,6 +511,7 @@ __device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int
 #pragma unroll
       for (int r = 0; r < R; ++r) d[r] = P::dw_row(xs[r], xs[r + 1], xs[r + 2], w);
       if (kc + 1 < NKC) load(kc + 1);
+      dw_mfma_fence<R>(d);
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
         DV a_nxt = a_cur;
@@ -951,6 +980,7 @@ struct EpiConv3 {
   bool first;
   Real act_h;             // active[b][u], loaded before the conv3 math
   int nb, nu, nfs;        // paired k_update: next item (nb < 0: none)
+  int pos_lo = 0;         // first strip position with an output row (RR blocks: kHalo)
 
   template <int R>
   __device__ void settle(PrefT<R>& pf) {
@@ -964,7 +994,9 @@ struct EpiConv3 {
   }
   __device__ void next_hook() const;
 
-  __device__ bool row_ok(int p, int t) const { return p < pos_hi && f_start + p < prm->a.F && t < kT; }
+  __device__ bool row_ok(int p, int t) const {
+    return p >= pos_lo && p < pos_hi && f_start + p < prm->a.F && t < kT;
+  }
 
   template <int R>
   __device__ void prefetch(PrefT<R>& pf, int p0, int t, int g) const {
@@ -1581,10 +1613,10 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
         for (int e = 0; e < P::EPC; ++e) {
           const int c = q * P::EPC + e;
           Real v = 0;
-          if (c < A2P) v = (Real)yv[c] * ns;
+          if (c < A2P) v = f32_rounded((Real)yv[c] * ns);
           else if (c == A2P) v = (Real)pv.x;
           else if (c == A2P + 1) v = (Real)pv.y;
-          else if (c < 2 * A2P + 2) v = (Real)hv[c - A2P - 2] * ns;
+          else if (c < 2 * A2P + 2) v = f32_rounded((Real)hv[c - A2P - 2] * ns);
           o[e] = (S)v;
         }
         *reinterpret_cast<intx4*>(X + xoff<P, NQZ>(lf, tt, q)) = *reinterpret_cast<const intx4*>(o);
@@ -1626,7 +1658,7 @@ __device__ intx4 g_zero16[1];
 // chunks of one slot); the chunk swizzle is applied on the source address (the lane at
 // physical chunk q' of symbol t loads logical chunk q' ^ swz(t)).  The pe chunk (2 values)
 // is written by ds_write after the DMA has landed.
-template <class P, int NW = 8>
+template <class P, int NW = 8, int W0 = (NRX_DMA_HI ? 8 - NW : 0)>
 __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X, int b, int u, int f_start) {
   using S = typename P::S;
   static_assert(sizeof(S) == 2 && kUPD_CINP * 2 / 16 == 16, "f16 z image with 16 chunks per symbol row");
@@ -1634,7 +1666,7 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
   // matches k's symbol group 4 (k & 3) + tq only when NW is a multiple of 4 and the issuing
   // waves w0 .. w0+NW-1 are 8-aligned as a set of residues mod 4
   static_assert(NW % 4 == 0 && NW <= 8, "DMA-issuing wave count must be 4 or 8");
-  static_assert(NRX_DMA_HI == 0 || NW == 4, "NRX_DMA_HI needs NW == 4");
+  static_assert(W0 % 4 == 0 && W0 + NW <= 8, "issuing waves: 0-3, 4-7 or all 8");
   constexpr int R0 = strip_slots<P>();
   constexpr int QS = kDS / P::EPC;   // 7 chunks of a, then 7 of s
   const auto& a = prm.a;
@@ -1660,9 +1692,8 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
       lsrc = sp + t * kDS + P::EPC * (q - QS);
     }
   }
-  // NRX_DMA_HI: the last NW waves issue instead of the first (same per-lane sources:
-  // the symbol group is wave & 3 either way)
-  const int w0 = NRX_DMA_HI ? 8 - NW : 0;
+  // W0: the first issuing wave (same per-lane sources: the symbol group is wave & 3 either way)
+  const int w0 = W0;
   if (wave < w0 || wave >= w0 + NW) return;
   for (int k = wave - w0; k < R0 * 4; k += NW) {
     const int f = f_start + (k >> 2);             // wave-uniform
@@ -1994,6 +2025,8 @@ __global__ __launch_bounds__(512) void k_update(BlockParams<P> prm) {
   stamp(5);
 }
 
+#include "nrx_rr.inc"
+
 // ======================================================================= launchers
 
 // CUs of the current device for the pairing / strip-tier heuristics, queried once per
@@ -2176,13 +2209,161 @@ static bool small_strips_fit(const FwdArgs<_Float16, float, _Float16>& a) {
   const long items = (long)a.B * a.U * ((a.F + P::FO - 1) / P::FO);
   return items <= cu_count() && (a.H + 1) * (kHeadSlot + 1024) <= strip_slots<P>() * slot_pitch<P>();
 }
+#ifndef NRX_RR
+#define NRX_RR 1
+#endif
+// NRX_RR in the environment (read at every forward): a bit mask of the launches that take
+// the register-resident kernels -- 1 StateInit, 2 aggregation-tail updates, 4 the readout
+// update; 0 = strip kernels everywhere (A/B runs, diagnostics).  Default 7.
+static int rr_mask() {
+  if (NRX_RR == 0) return 0;
+  const char* e = getenv("NRX_RR");
+  return e ? atoi(e) : 7;
+}
+
+// Register-resident path (nrx_rr.inc): throughput tier (more items than CUs), StateInit
+// antenna padding A2P <= 16, U <= 2 (the update z image is an LDS-DMA copy).  The readout
+// launch runs RR when its heads fit BB (one LLR head, 2A <= 16), else the strip kernel's
+// unpaired readout.  Same HBM state layout as the strip kernels: launches mix freely.
+static bool rr_applicable(const FwdArgs<_Float16, float, _Float16>& a, const RrImages* rr) {
+  if (!rr || rr_mask() == 0) return false;
+  const long items = (long)a.B * a.U * ((a.F + PRR::FO - 1) / PRR::FO);
+  return items > cu_count() && 2 * a.A <= 16 && a.U <= 2 && rr->upd[0][0] != nullptr;
+}
+
+// BlockParams of the strip kernels (FO = 24) for one launch of a mixed RR / strip forward
+static BlockParams<P16> strip_params(const BlockParams<PRR>& q, const ModelW<_Float16, float>& W) {
+  BlockParams<P16> bp{};
+  bp.a = q.a;
+  bp.inline_combine = 1;
+  bp.pair = 0;
+  bp.strips = (q.a.F + P16::FO - 1) / P16::FO;
+  bp.norm_pre = q.norm_pre;
+  bp.order_rev = q.order_rev;
+  bp.m = q.m;
+  bp.tail = q.tail;
+  for (int l = 0; l < 3; ++l) bp.w[l] = q.w[l];
+  bp.agg[0] = q.agg[0];
+  bp.agg[1] = q.agg[1];
+  for (int h = 0; h < q.a.H; ++h) {
+    bp.llr[h][0] = W.llr[h][0];
+    bp.llr[h][1] = W.llr[h][1];
+  }
+  bp.chest[0] = W.chest[0];
+  bp.chest[1] = W.chest[1];
+  return bp;
+}
+
+static hipError_t run_rr(const FwdArgs<_Float16, float, _Float16>& args0, const ModelW<_Float16, float>& W,
+                         const RrImages& rr, int num_it, hipStream_t st, Prof* prof) {
+  const int mask = rr_mask();
+  constexpr int L16 = strip_lds_bytes<P16>();
+  FwdArgs<_Float16, float, _Float16> args = args0;
+  auto B_ = [&](int k) { if (prof) prof->begin(k, st); };
+  auto E_ = [&](int k) { if (prof) prof->end(k, st); };
+  const int strips = (args.F + PRR::FO - 1) / PRR::FO;
+  const int items = args.B * args.U * strips;
+  const int cus = cu_count();
+  RrParams p{};
+  p.bp.a = args;
+  p.bp.inline_combine = 1;
+  p.bp.pair = 0;
+  p.bp.strips = strips;
+  p.items = items;
+  p.per_wg = (items + cus - 1) / cus;
+  int grid = (items + p.per_wg - 1) / p.per_wg;
+  if (grid % 8 && (grid + 7) / 8 * 8 <= cus) grid = (grid + 7) / 8 * 8;   // XCD grouping of work_item
+  for (int h = 0; h < args.H; ++h) {
+    p.bp.llr[h][0] = W.llr[h][0];
+    p.bp.llr[h][1] = W.llr[h][1];
+  }
+  p.bp.chest[0] = W.chest[0];
+  p.bp.chest[1] = W.chest[1];
+  const int nq = args.F * kT * 2 * args.A / 4;
+  p.bp.norm_pre = nq > kNormFusedMaxQ;
+  if (p.bp.norm_pre) {
+    B_(K_NORM);
+    k_norm<<<args.B, 1024, 0, st>>>(args.y, nq, args.norm);
+    E_(K_NORM);
+  }
+  int launch_no = 0;
+  B_(K_INIT);
+  for (int m = 0; m < args.num_init; ++m) {
+    for (int l = 0; l < 3; ++l) {
+      p.bp.w[l] = W.init[m][l];
+      p.w_img[l] = rr.init[m][l];
+    }
+    p.bp.m = m;
+    const bool tl = m == args.num_init - 1;
+    p.bp.tail = tl ? TAIL_AGG : TAIL_NONE;
+    p.bp.agg[0] = W.agg[0][0];
+    p.bp.agg[1] = W.agg[0][1];
+    p.tail_img = rr.tail[0];
+    p.tail_bytes = kRrTailBytes;
+    p.bp.order_rev = launch_no++ & 1;
+    if (!(mask & 1)) {
+      BlockParams<P16> bp = strip_params(p.bp, W);
+      const dim3 g16(bp.strips * args.U * args.B);
+      if (2 * args.A <= 8) Launch<P16>::launch_init<8>(g16, L16, st, bp, tl);
+      else Launch<P16>::launch_init<16>(g16, L16, st, bp, tl);
+    } else if (2 * args.A <= 8) {
+      if (tl) k_init_rr<TAIL_AGG, 8><<<grid, 512, kRrLds, st>>>(p);
+      else k_init_rr<TAIL_NONE, 8><<<grid, 512, kRrLds, st>>>(p);
+    } else {
+      if (tl) k_init_rr<TAIL_AGG, 16><<<grid, 512, kRrLds, st>>>(p);
+      else k_init_rr<TAIL_NONE, 16><<<grid, 512, kRrLds, st>>>(p);
+    }
+  }
+  E_(K_INIT);
+  const bool ro_rr = args.H == 1 && rr.heads && rr.heads_bytes <= kRrBBytes;
+  for (int i = 0; i < num_it; ++i) {
+    std::swap(p.bp.a.s_in, p.bp.a.s_out);
+    std::swap(p.bp.a.a, p.bp.a.a_out);
+    for (int l = 0; l < 3; ++l) {
+      p.bp.w[l] = W.upd[i][l];
+      p.w_img[l] = rr.upd[i][l];
+    }
+    const bool last = i == num_it - 1;
+    p.bp.order_rev = launch_no++ & 1;
+    B_(K_UPDATE);
+    if (!last) {
+      p.bp.tail = TAIL_AGG;
+      p.bp.agg[0] = W.agg[i + 1][0];
+      p.bp.agg[1] = W.agg[i + 1][1];
+      p.tail_img = rr.tail[i + 1];
+      p.tail_bytes = kRrTailBytes;
+      if (mask & 2) {
+        k_update_rr<TAIL_AGG><<<grid, 512, kRrLds, st>>>(p);
+      } else {
+        BlockParams<P16> bp = strip_params(p.bp, W);
+        k_update<P16, 16, TAIL_AGG><<<dim3(bp.strips * args.U * args.B), 512, L16, st>>>(bp);
+      }
+    } else if (ro_rr && (mask & 4)) {
+      p.bp.tail = TAIL_READOUT_WB;
+      p.tail_img = rr.heads;
+      p.tail_bytes = rr.heads_bytes;
+      k_update_rr<TAIL_READOUT_WB><<<grid, 512, kRrLds, st>>>(p);
+    } else {
+      // strip kernel readout (several LLR heads, or heads wider than BB)
+      p.bp.tail = TAIL_READOUT;
+      BlockParams<P16> bp = strip_params(p.bp, W);
+      const dim3 g16(bp.strips * args.U * args.B);
+      constexpr int L = L16;
+      k_update<P16, 16, TAIL_READOUT><<<g16, 512, L, st>>>(bp);
+    }
+    E_(K_UPDATE);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args,
-                              const ModelW<_Float16, float>& W, int num_it, hipStream_t st,
+                              const ModelW<_Float16, float>& W, const RrImages* rr, int num_it, hipStream_t st,
                               Prof* prof) {
   if (NRX_SMALL_STRIPS != 0) {
     if (small_strips_fit<P16S>(args)) return Launch<P16S>::run(args, W, num_it, st, prof);
     if (small_strips_fit<P16M>(args)) return Launch<P16M>::run(args, W, num_it, st, prof);
   }
+  if (rr_applicable(args, rr)) return run_rr(args, W, *rr, num_it, st, prof);
   return Launch<P16>::run(args, W, num_it, st, prof);
 }
 
@@ -2197,6 +2378,15 @@ hipError_t setup_kernels() {
   hipError_t e = Launch<P16>::setup();
   hipError_t e1 = Launch<P16S>::setup();
   if (e1 == hipSuccess) e1 = Launch<P16M>::setup();
+  if (e1 == hipSuccess) {
+    const void* fs[] = {(const void*)k_init_rr<TAIL_AGG, 8>, (const void*)k_init_rr<TAIL_NONE, 8>,
+                        (const void*)k_init_rr<TAIL_AGG, 16>, (const void*)k_init_rr<TAIL_NONE, 16>,
+                        (const void*)k_update_rr<TAIL_AGG>, (const void*)k_update_rr<TAIL_READOUT_WB>};
+    for (const void* f : fs) {
+      hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kRrLds);
+      if (r != hipSuccess) e1 = r;
+    }
+  }
   hipError_t e2 = Launch<P64>::setup();
   return e != hipSuccess ? e : (e1 != hipSuccess ? e1 : e2);
 }

@@ -183,10 +183,16 @@ def test_batch_composition_invariance_paired_items(name):
     llr, h = eng.forward(t(case.y), t(case.pe), t(case.h_hat), t(case.active),
                          t(case.mcs_mask) if multi else None, None, "f16")
     B = kw["batch"]
-    sel = sorted({0, 5 % B, 77 % B, B - 1})
-    llr4, h4 = eng.forward(t(case.y[sel]), t(case.pe), t(case.h_hat[sel]), t(case.active[sel]),
-                           t(case.mcs_mask[sel]) if multi else None, None, "f16")
-    torch.cuda.synchronize()
-    assert np.array_equal(llr.cpu().numpy()[:, sel], llr4.cpu().numpy())
-    assert np.array_equal(h.cpu().numpy()[sel], h4.cpu().numpy())
-    assert np.isfinite(llr.cpu().numpy()).all()
+    llr_np, h_np = llr.cpu().numpy(), h.cpu().numpy()
+    assert np.isfinite(llr_np).all()
+    bad = []
+    # every slot, 4 at a time (each 4-slot run stays in the small-strip tier)
+    for s0 in range(0, B, 4):
+        sel = list(range(s0, min(s0 + 4, B)))
+        llr4, h4 = eng.forward(t(case.y[sel]), t(case.pe), t(case.h_hat[sel]), t(case.active[sel]),
+                               t(case.mcs_mask[sel]) if multi else None, None, "f16")
+        l4, hh4 = llr4.cpu().numpy(), h4.cpu().numpy()
+        for i, b in enumerate(sel):
+            if not (np.array_equal(llr_np[:, b], l4[:, i]) and np.array_equal(h_np[b], hh4[i])):
+                bad.append(b)
+    assert not bad, f"slots whose outputs depend on the batch: {bad}"

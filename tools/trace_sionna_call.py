@@ -13,9 +13,9 @@ from neural_rx_amd.receiver import NeuralReceiver
 from tests.helpers import make_case
 
 case = make_case("nrx_rt", batch=4, users=2, prbs=4, snr_db=12, seed=41)
-yc = torch.from_numpy(case.slots.y_complex).cuda()
-h = torch.from_numpy(case.h_hat).cuda()
-act = torch.from_numpy(case.active).cuda()
+yc = torch.from_numpy(np.ascontiguousarray(case.slots.y_complex)).cuda()
+h = torch.from_numpy(np.ascontiguousarray(case.h_hat)).cuda()
+act = torch.from_numpy(np.ascontiguousarray(case.active)).cuda()
 nrx = NeuralReceiver("nrx_rt")
 pe = nrx.positional_encoding(2, 48)
 torch.cuda.synchronize()
