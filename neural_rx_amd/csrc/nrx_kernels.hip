@@ -69,9 +69,19 @@ __device__ __forceinline__ void stamp_w(int k) {
     if (wg < 4096) g_nrx_stamps[wg][k + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime();
   }
 }
+// register-resident kernels (own array): phase ph (0..31) of the workgroup's item ks == 1,
+// for wave 0 (R = 3, no DMA duty) and wave 4 (R = 2, DMA issuer) of the same SIMD
+__device__ unsigned long long g_nrx_rr_stamps[4096][64];
+__device__ __forceinline__ void rr_stamp(int ks, int ph) {
+  if (ks == 1 && (threadIdx.x & 255) == 0 && g_nrx_stamp_on) {
+    const int wg = blockIdx.x;
+    if (wg < 4096) g_nrx_rr_stamps[wg][ph * 2 + (threadIdx.x >> 8)] = __builtin_amdgcn_s_memtime();
+  }
+}
 #else
 __device__ __forceinline__ void stamp(int) {}
 __device__ __forceinline__ void stamp_w(int) {}
+__device__ __forceinline__ void rr_stamp(int, int) {}
 #endif
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -108,31 +118,6 @@ __device__ __forceinline__ float f32_rounded(float v) {
   return v;
 }
 __device__ __forceinline__ double f32_rounded(double v) { return v; }
-
-// The depthwise results are written by inline-asm DPP FMAs, whose latency the compiler's
-// hazard recognizer does not model: an MFMA that reads one as its B operand right behind
-// the last FMA can read the register before the write lands (seen as a wrong first output
-// tile of the last row of a 2-row pass).  This fence sits between the depthwise of a K
-// chunk and its MFMAs (the d values flow through it) and pads the VALU -> MFMA-operand
-// wait states.
-template <int R>
-__device__ __forceinline__ void dw_mfma_fence(half8 (&d)[R]) {
-  if constexpr (R == 1) asm volatile("s_nop 3" : "+v"(d[0]));
-  else if constexpr (R == 2) asm volatile("s_nop 3" : "+v"(d[0]), "+v"(d[1]));
-  else if constexpr (R == 3) asm volatile("s_nop 3" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]));
-  else asm volatile("s_nop 3" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]));
-}
-template <int R>
-__device__ __forceinline__ void dw_mfma_fence(doublex4 (&)[R]) {}
-// Same for the depthwise's DPP source rows when they are VALU results (z rows converted in
-// registers, the previous layer's outputs): a VALU write needs two wait states before a DPP
-// reads the register, which the compiler does not insert in front of inline asm.
-template <int N>
-__device__ __forceinline__ void dw_src_fence(half8 (&x)[N]) {
-  if constexpr (N == 3) asm volatile("s_nop 1" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]));
-  else if constexpr (N == 4) asm volatile("s_nop 1" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]));
-  else asm volatile("s_nop 1" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]));
-}
 
 __device__ __forceinline__ half2 h2(half8 v, int k) {
   return half2{v[2 * k], v[2 * k + 1]};
@@ -175,7 +160,7 @@ struct P16T {
   __device__ static DV dw_row(DV x0, DV x1, DV x2, const DV (&w)[9]) {
     // the centre column's contraction is fixed in the source (not left to the compiler,
     // which contracted it differently in different kernels: 1-ulp differences between
-    // strip widths / kernel families)
+    // kernel families); the six side taps are inline-asm DPP FMACs on top of it
     const DV c = __builtin_elementwise_fma(w[7], x2, __builtin_elementwise_fma(w[4], x1, w[1] * x0));
     half2 d[4];
 #pragma unroll
@@ -511,7 +496,6 @@ __device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int
 #pragma unroll
       for (int r = 0; r < R; ++r) d[r] = P::dw_row(xs[r], xs[r + 1], xs[r + 2], w);
       if (kc + 1 < NKC) load(kc + 1);
-      dw_mfma_fence<R>(d);
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
         DV a_nxt = a_cur;
@@ -2214,11 +2198,13 @@ static bool small_strips_fit(const FwdArgs<_Float16, float, _Float16>& a) {
 #endif
 // NRX_RR in the environment (read at every forward): a bit mask of the launches that take
 // the register-resident kernels -- 1 StateInit, 2 aggregation-tail updates, 4 the readout
-// update; 0 = strip kernels everywhere (A/B runs, diagnostics).  Default 7.
+// update.  Default 0 (strip kernels everywhere): measured on the bench shape the RR kernels
+// run 53.5 / 53.5 / 60.6 us against the strip kernels' 43.5 / 45.2 / 35.6 us (same box,
+// profiles/r03/README.md), so they stay an opt-in path, bit-identical to the strip kernels.
 static int rr_mask() {
   if (NRX_RR == 0) return 0;
   const char* e = getenv("NRX_RR");
-  return e ? atoi(e) : 7;
+  return e ? atoi(e) : 0;
 }
 
 // Register-resident path (nrx_rr.inc): throughput tier (more items than CUs), StateInit
@@ -2287,8 +2273,21 @@ static hipError_t run_rr(const FwdArgs<_Float16, float, _Float16>& args0, const 
     E_(K_NORM);
   }
   int launch_no = 0;
+  // diagnostic builds: NRX_STAMP_LAUNCH selects the launch that records (-1 - m: StateInit m,
+  // i: update i)
+  auto stamp_sel = [&](int id) {
+#ifdef NRX_STAMPS
+    static const int sel = getenv("NRX_STAMP_LAUNCH") ? atoi(getenv("NRX_STAMP_LAUNCH")) : 0;
+    const int on = sel == id;
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_nrx_stamp_on), &on, sizeof(int), 0, hipMemcpyHostToDevice, st);
+    (void)hipStreamSynchronize(st);
+#else
+    (void)id;
+#endif
+  };
   B_(K_INIT);
   for (int m = 0; m < args.num_init; ++m) {
+    stamp_sel(-1 - m);
     for (int l = 0; l < 3; ++l) {
       p.bp.w[l] = W.init[m][l];
       p.w_img[l] = rr.init[m][l];
@@ -2325,6 +2324,7 @@ static hipError_t run_rr(const FwdArgs<_Float16, float, _Float16>& args0, const 
     }
     const bool last = i == num_it - 1;
     p.bp.order_rev = launch_no++ & 1;
+    stamp_sel(i);
     B_(K_UPDATE);
     if (!last) {
       p.bp.tail = TAIL_AGG;
@@ -2396,6 +2396,9 @@ int strip_width(int precision) { return precision == 0 ? P16::FO : P64::FO; }
 #ifdef NRX_STAMPS
 extern "C" int nrx_debug_stamps(void* out, int n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nrx_stamps), (size_t)n * 64 * 8, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int nrx_debug_rr_stamps(void* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nrx_rr_stamps), (size_t)n * 64 * 8, 0, hipMemcpyDeviceToHost);
 }
 #endif
 
