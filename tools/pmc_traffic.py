@@ -32,7 +32,7 @@ def per_kernel(d, counter):
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
-def main(fdir, wdir, key, num_it=2):
+def main(fdir, wdir, key, source=None, num_it=2):
     fe, wr = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
     out = {}
     for k in fe:
@@ -44,6 +44,8 @@ def main(fdir, wdir, key, num_it=2):
     upd_last = [v["bytes"] for k, v in out.items() if k.startswith("nrx::k_update") and k.endswith((", 1>", ", 2>"))]
     rec = {"kernels": out, "unit": "bytes per launch",
            "note": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), rocprofv3 separate --pmc passes"}
+    if source:
+        rec["source"] = source
     if upd_mid and upd_last:
         rec["k_update_bytes_per_launch"] = round(((num_it - 1) * upd_mid[0] + upd_last[0]) / num_it)
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -54,4 +56,4 @@ def main(fdir, wdir, key, num_it=2):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3])
+    main(sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else None)
