@@ -14,7 +14,8 @@ all-reduce of the per-rank elapsed time (MAX) after the timed region.
 
 Prints ONE JSON line (rank 0) with the headline metric (slots/s, whole job), the
 per-slot p50 latency at batch 1, the roofline of the dominant kernel
-(state update, measured with HIP events on the launch stream) and a CPU baseline
+(the one-launch forward k_forward at this shape -- the state-update launch where the
+three-launch path runs -- measured with HIP events on the launch stream) and a CPU baseline
 (the torch-CPU restatement, fp32, BASELINE.md's plan: cfg1 latency and cfg2 throughput at
 all threads and at 1 thread, on a bounded sample on this host).
 """
@@ -176,31 +177,46 @@ def main():
             kern[name] = {"launches": n, "avg_us": round(avg_s * 1e6, 3),
                           "avg_us_event_pairs": round(ms / n * 1e3, 3),
                           "tflops": round(fl / avg_s / 1e12, 2) if fl else None}
-    dom = "state_update"
+    fused = prof.get("forward", (0, 0.0))[0] > 0
+    # the dominant kernel: the one-launch forward when the engine took it (throughput tier),
+    # else the state-update launch of the three-launch forward
+    dom = "forward" if fused else "state_update"
     dom_avg_s = prof[dom][1] / prof[dom][0] * 1e-3 * scale
     dom_flops = kflops[dom] * re_users
     peak = metrics.PEAK_TFLOPS[args.precision]
     achieved = dom_flops / dom_avg_s / 1e12
+    elem = 2 if args.precision == "f16" else 4
+    if fused:
+        alg_bytes = metrics.forward_bytes_per_re_user(spec, num_it, U, elem) * re_users
+        pmc_field, kname = "k_forward_bytes_per_launch", \
+            "k_forward (StateInit + num_it state updates + readouts: one persistent launch)"
+        mixed = metrics.forward_mixed_bound_tflops(spec, num_it, peak) if args.precision == "f16" else None
+        mixed_note = ("the forward's depthwise FLOPs at the VALU peak (157 TF) + its dense FLOPs at the "
+                      "f16 MFMA peak, pipes overlapped (metrics.forward_mixed_bound_tflops)")
+    else:
+        alg_bytes = metrics.update_launch_bytes_per_re_user(spec, num_it, elem) * re_users
+        pmc_field, kname = "k_update_bytes_per_launch", "k_update (3 sep-convs + fused aggregation/readout tail)"
+        mixed = metrics.mixed_bound_tflops(spec, num_it, peak) if args.precision == "f16" else None
+        mixed_note = ("k_update's depthwise FLOPs at the VALU peak (157 TF) + its dense FLOPs at the f16 "
+                      "MFMA peak, pipes overlapped (metrics.mixed_bound_tflops)")
     traffic = None
     pmc, key = {}, f"{args.config}_b{B}_u{U}_p{args.prbs}_{args.precision}"
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
-            traffic = pmc.get(key, {}).get("k_update_bytes_per_launch")
+            traffic = pmc.get(key, {}).get(pmc_field)
         except Exception:
             traffic = None
     pmc_src = None
     if traffic is not None:
         pmc_src = pmc.get(key, {}).get("source")
     whole_tflops = metrics.forward_flops_per_re_user(spec, num_it) * re_users * world / (elapsed / args.steps) / 1e12
-    mixed = metrics.mixed_bound_tflops(spec, num_it, peak) if args.precision == "f16" else None
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
-                "kernel": "k_update (3 sep-convs + fused aggregation/readout tail)",
+                "kernel": kname,
                 "flops_per_launch": dom_flops,
-                "algorithmic_bytes_per_launch": round(metrics.update_launch_bytes_per_re_user(
-                    spec, num_it, 2 if args.precision == "f16" else 4) * re_users),
+                "algorithmic_bytes_per_launch": round(alg_bytes),
                 "avg_launch_us": round(dom_avg_s * 1e6, 3),
                 "avg_launch_us_event_pairs": kern[dom]["avg_us_event_pairs"],
                 "avg_launch_us_kind": "derived: event-pair share of a step x uninstrumented step time",
@@ -212,8 +228,7 @@ def main():
                 "whole_forward_frac": round(whole_tflops / world / peak, 4),
                 "mixed_bound_tflops": round(mixed, 1) if mixed else None,
                 "frac_of_mixed_bound": round(achieved / mixed, 4) if mixed else None,
-                "mixed_bound_note": "k_update's depthwise FLOPs at the VALU peak (157 TF) + its dense FLOPs "
-                                    "at the f16 MFMA peak, pipes overlapped (metrics.mixed_bound_tflops)",
+                "mixed_bound_note": mixed_note,
                 "traffic_source": pmc_src}
 
     # ---- batch-1 per-slot latency (hipGraph replay; device-only and H2D+compute+D2H)

@@ -279,11 +279,21 @@ double nrx_flops_per_re_user(const nrx_desc* desc, int32_t num_it);
 /* Per-kernel timing.  While enabled, nrx_forward records a HIP event pair around
  * every kernel launch on the launch stream (not graph-capture safe).  Kernel ids:
  * 0 norm, 1 state-init (+ fused aggregation tail), 2 state-update (+ fused aggregation
- * or readout tail).
+ * or readout tail), 3 the one-launch forward (StateInit + updates + readouts; taken for
+ * the throughput tier, see nrx_fused_status).
  * nrx_profile_enable(h, 1) (re)starts the counters; nrx_profile_read waits for the
  * recorded events and returns the launch count and summed device time of a kernel. */
 int nrx_profile_enable(nrx_handle* h, int32_t enable);
 int nrx_profile_read(nrx_handle* h, int32_t kernel, int64_t* launches, double* total_ms);
+
+/* The throughput tier of nrx_forward (f16, 24-row strips, >= 2 items per CU, U <= 2, one
+ * StateInit, one LLR head) runs the whole forward as ONE persistent launch whose items wait
+ * on per-(stage, slot) counters in a handle-owned buffer.  Its waits are bounded; *error is
+ * set to 1 (sticky) if one ever timed out (results of that forward are then invalid).
+ * Blocking; reset != 0 clears the word.  Forwards on one handle must not run concurrently
+ * on several streams (the counters are per handle).  NRX_FUSED=0 in the environment takes
+ * the three-launch path instead. */
+int nrx_fused_status(nrx_handle* h, int32_t* error, int32_t reset);
 
 const char* nrx_last_error(void);
 int32_t nrx_api_version(void);

@@ -25,11 +25,11 @@ EXPORTS = [
     "nrx_compute_pe", "nrx_flops_per_re_user", "nrx_last_error", "nrx_api_version",
     "nrx_profile_enable", "nrx_profile_read", "nrx_aerial_workspace_size", "nrx_forward_aerial",
     "nrx_llr_demap", "nrx_gen_workspace_size", "nrx_generate_slots", "nrx_count_errors",
-    "nrx_workspace_size_ex", "nrx_forward_ex",
+    "nrx_workspace_size_ex", "nrx_forward_ex", "nrx_fused_status",
 ]
 # enum nrx_y_layout
 Y_LAYOUTS = {"cgnn": 0, "sionna": 1, "split": 2}
-KERNELS = ["norm", "state_init", "state_update"]
+KERNELS = ["norm", "state_init", "state_update", "forward"]
 
 
 class NRXLibraryError(RuntimeError):
@@ -217,6 +217,8 @@ def load(path: str = LIB_PATH):
     lib.nrx_profile_enable.restype = c.c_int
     lib.nrx_profile_read.argtypes = [c.c_void_p, c.c_int32, P(c.c_int64), P(c.c_double)]
     lib.nrx_profile_read.restype = c.c_int
+    lib.nrx_fused_status.argtypes = [c.c_void_p, P(c.c_int32), c.c_int32]
+    lib.nrx_fused_status.restype = c.c_int
     lib.nrx_aerial_workspace_size.argtypes = [c.c_void_p, P(nrx_aerial_io), P(c.c_size_t)]
     lib.nrx_aerial_workspace_size.restype = c.c_int
     lib.nrx_forward_aerial.argtypes = [c.c_void_p, P(nrx_aerial_io), c.c_void_p, c.c_size_t, c.c_void_p]

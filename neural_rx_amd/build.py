@@ -40,11 +40,28 @@ def build(force: bool = False, verbose: bool = True) -> str:
         return LIB
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     tmp = LIB + f".tmp{os.getpid()}"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", *SOURCES, "-o", tmp]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+    # one object per source, compiled in parallel (nrx_kernels.hip dominates), then one link
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = os.path.join(os.path.dirname(LIB), os.path.basename(src) + f".{os.getpid()}.o")
+        cmd = [hipcc(), *flags, "-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        objs.append(obj)
+        procs.append(subprocess.Popen(cmd))
+    bad = [p.wait() for p in procs]
+    try:
+        if any(bad):
+            raise subprocess.CalledProcessError(max(bad), "hipcc -c")
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", *objs, "-o", tmp]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    finally:
+        for o in objs:
+            if os.path.exists(o):
+                os.remove(o)
     os.replace(tmp, LIB)
     return LIB
 

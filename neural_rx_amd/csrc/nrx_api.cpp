@@ -20,7 +20,9 @@
 
 namespace nrx {
 hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args, const ModelW<_Float16, float>& W,
-                              const RrImages* rr, int num_it, hipStream_t st, Prof* prof);
+                              const RrImages* rr, int num_it, hipStream_t st, Prof* prof, void* fused_sync);
+size_t fused_sync_bytes();
+hipError_t fused_sync_status(void* sync, int* err, bool reset);
 hipError_t launch_forward_f64(const FwdArgs<double, double, float>& args,
                               const ModelW<double, double>& W, int num_it, hipStream_t st,
                               Prof* prof);
@@ -430,6 +432,7 @@ struct nrx_handle {
   DeviceModel<_Float16, float> m16;
   DeviceModel<double, double> m64;
   EventProf* prof = nullptr;
+  void* fused_sync = nullptr;   // k_forward's work queues and dependency counters (zeroed)
 };
 
 static size_t state_bytes(const nrx_shape* s, int precision) {
@@ -520,6 +523,12 @@ int nrx_create(const nrx_desc* desc, const float* const* weights, const int64_t*
   nrx_handle* h = new nrx_handle();
   h->desc = *desc;
   h->device = device;
+  e = hipMalloc(&h->fused_sync, fused_sync_bytes());
+  if (e == hipSuccess) e = hipMemset(h->fused_sync, 0, fused_sync_bytes());
+  if (e != hipSuccess) {
+    nrx_destroy(h);
+    return hip_fail(e, "fused forward counters");
+  }
   rc = build_model<_Float16, float>(desc, weights, 32, &h->m16);
   if (!rc) rc = build_model<double, double>(desc, weights, 16, &h->m64);
   if (rc) {
@@ -535,6 +544,7 @@ void nrx_destroy(nrx_handle* h) {
   if (h->m16.dev) (void)hipFree(h->m16.dev);
   if (h->m16.rr_dev) (void)hipFree(h->m16.rr_dev);
   if (h->m64.dev) (void)hipFree(h->m64.dev);
+  if (h->fused_sync) (void)hipFree(h->fused_sync);
   delete h->prof;
   delete h;
 }
@@ -567,7 +577,7 @@ int nrx_forward(nrx_handle* h, const nrx_io* io, void* workspace, size_t workspa
   if (io->precision == NRX_PREC_F16) {
     FwdArgs<_Float16, float, _Float16> a{};
     fill_args(a, h, io, workspace, h->m16.init_cinp);
-    e = launch_forward_f16(a, h->m16.W, &h->m16.rr, io->num_it, st, h->prof);
+    e = launch_forward_f16(a, h->m16.W, &h->m16.rr, io->num_it, st, h->prof, h->fused_sync);
   } else {
     FwdArgs<double, double, float> a{};
     fill_args(a, h, io, workspace, h->m64.init_cinp);
@@ -814,6 +824,15 @@ int nrx_profile_enable(nrx_handle* h, int32_t enable) {
     delete h->prof;
     h->prof = nullptr;
   }
+  return NRX_OK;
+}
+
+int nrx_fused_status(nrx_handle* h, int32_t* error, int32_t reset) {
+  if (!h || !error) return fail(NRX_ERR_INVALID_ARG, "null argument");
+  int err = 0;
+  hipError_t e = fused_sync_status(h->fused_sync, &err, reset != 0);
+  if (e != hipSuccess) return hip_fail(e, "fused status");
+  *error = err;
   return NRX_OK;
 }
 

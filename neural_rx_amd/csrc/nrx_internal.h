@@ -119,7 +119,7 @@ struct FwdArgs {
 
 // Optional per-kernel timing (nrx_profile_enable): events recorded around each launch on
 // the launch stream.  Kernel ids:
-enum KernelId { K_NORM = 0, K_INIT = 1, K_UPDATE = 2, K_COUNT = 3 };
+enum KernelId { K_NORM = 0, K_INIT = 1, K_UPDATE = 2, K_FUSED = 3, K_COUNT = 4 };
 
 struct Prof {
   virtual void begin(int kid, void* stream) = 0;

@@ -92,6 +92,16 @@ typedef double doublex4 __attribute__((ext_vector_type(4)));
 typedef int intx4 __attribute__((ext_vector_type(4)));
 typedef int intx8 __attribute__((ext_vector_type(8)));
 
+// Work-item id as an opaque value (one volatile asm per use): the one-launch forward runs
+// the item code inside a loop, and LLVM's LICM hoisted every thread-index-derived address of
+// every item body out of it -- ~70 values live across the whole loop, spilled to scratch and
+// reloaded in the conv loops.  An opaque id per use keeps each derivation where it is used.
+__device__ __forceinline__ unsigned nrx_tid() {
+  unsigned t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 // DPP: lane l receives lane l-1 (row_shr:1) / lane l+1 (row_shl:1) inside its 16-lane
 // row; the lane without a source gets 0 (bound_ctrl).
 __device__ __forceinline__ int dpp_shr1(int v) {
@@ -359,7 +369,7 @@ struct SepStage {
   intx4 v[PER];
   intx4 vx;
   __device__ void load(const SepW<_Float16, float>& w) {
-    const int tid = threadIdx.x;
+    const int tid = nrx_tid();
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int idx = tid + i * 512;
@@ -370,7 +380,7 @@ struct SepStage {
     else if (tid - NDW < NB) vx = reinterpret_cast<const intx4*>(w.b)[tid - NDW];
   }
   __device__ void store(char* wb) const {
-    const int tid = threadIdx.x;
+    const int tid = nrx_tid();
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int idx = tid + i * 512;
@@ -395,21 +405,21 @@ struct DenseStage {
   __device__ void load(const DenseW<_Float16, float>& w) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int idx = threadIdx.x + i * 512;
+      const int idx = nrx_tid() + i * 512;
       if (idx < NW) v[i] = *reinterpret_cast<const intx4*>(w.w + (idx / NQ) * CINP + (idx % NQ) * 8);
     }
-    bias = threadIdx.x < COUTP ? w.b[threadIdx.x] : 0.f;
+    bias = nrx_tid() < COUTP ? w.b[nrx_tid()] : 0.f;
   }
   __device__ void store(char* dst, float* bias_dst, int rows = COUTP) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int idx = threadIdx.x + i * 512;
+      const int idx = nrx_tid() + i * 512;
       if (idx < NW && idx / NQ < rows) {
         const int co = idx / NQ, q = idx % NQ;
         *reinterpret_cast<intx4*>(dst + lds_off<NQ>(co >> 4, co & 15, q)) = v[i];
       }
     }
-    if (threadIdx.x < COUTP) bias_dst[threadIdx.x] = bias;
+    if (nrx_tid() < COUTP) bias_dst[nrx_tid()] = bias;
   }
 };
 
@@ -526,12 +536,13 @@ template <class P, int CINP, int COUTP, int R, class WS, class Epi, class Post>
 __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off, int p0, bool act, bool first_round,
                                            const WS& ws, Epi& epi, Post& post_math) {
   using E = std::decay_t<Epi>;
-  const int lane = threadIdx.x & 63;
+  const int lane = nrx_tid() & 63;
   const int t = lane & 15, g = lane >> 4;
   typename P::Acc acc[R][COUTP / 16];
   typename E::template PrefT<R> pf;
   stamp(8 + 5 * in_off);
   if (act) epi.template prefetch<R>(pf, p0, t, g);   // epilogue global loads, in flight during the math
+  if constexpr (E::kNextHook || E::kNextHookRO) epi.poll();
   if (act) {
     if constexpr (NRX_ABLATE & 1) {
 #pragma unroll
@@ -601,7 +612,7 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
 template <class P, int CINP, int COUTP, class WS, class Epi, class Post>
 __device__ __forceinline__ void conv_layer(const char* X, int nslots, int in_off, int pos_lo,
                                            int pos_hi, const WS& ws, Epi&& epi, Post&& post_math) {
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane(nrx_tid() >> 6);
   if constexpr (P::WLDS) {
     static_assert(P::R == 4, "f16 row split assumes passes of 4 / 3 rows");
     const int nrows = pos_hi - pos_lo;   // <= 32 (static_assert on FO)
@@ -857,12 +868,12 @@ template <int CINP, int COUTP>
 __device__ __forceinline__ void stage_dense(char* dst, float* bias_dst, const DenseW<_Float16, float>& w) {
   constexpr int NQ = CINP * 2 / 16;
   constexpr int NW = COUTP * NQ;
-  for (int idx = threadIdx.x; idx < NW; idx += 512) {
+  for (int idx = nrx_tid(); idx < NW; idx += 512) {
     const int co = idx / NQ, q = idx % NQ;
     *reinterpret_cast<intx4*>(dst + lds_off<NQ>(co >> 4, co & 15, q)) =
         *reinterpret_cast<const intx4*>(w.w + co * CINP + q * 8);
   }
-  for (int idx = threadIdx.x; idx < COUTP; idx += 512) bias_dst[idx] = w.b[idx];
+  for (int idx = nrx_tid(); idx < COUTP; idx += 512) bias_dst[idx] = w.b[idx];
 }
 
 // B fragments of a dense layer whose input is NT accumulator tiles in C layout.
@@ -965,6 +976,27 @@ struct EpiConv3 {
   Real act_h;             // active[b][u], loaded before the conv3 math
   int nb, nu, nfs;        // paired k_update: next item (nb < 0: none)
   int pos_lo = 0;         // first strip position with an output row (RR blocks: kHalo)
+  // fused forward (k_forward): the next item belongs to stage nprm and may start only once
+  // its dependency counter ndone has reached nneed.  The counter is polled at the start of
+  // the conv3 layer (poll), its value is read after the math (settle), and the next z DMA is
+  // issued only when it was complete (nflag, LDS).  ndone == nullptr: no dependency (paired
+  // items of one launch).
+  const BlockParams<P>* nprm = nullptr;
+  const int* ndone = nullptr;
+  int nneed = 0;
+  int* nflag = nullptr;
+  int npoll = 0;
+
+  // wave 0 lane 0: the dependency counter of the next item (sc1 load: L2-served), then an
+  // agent-scope L1 invalidate, so that no line of the next item's inputs this CU read in an
+  // earlier stage (ping-pong buffers) is still valid when its z DMA and skip rows load them.
+  // Both complete asynchronously behind the conv3 math; settle waits for them.
+  __device__ void poll() {
+    if (ndone && nrx_tid() == 0) {
+      npoll = __hip_atomic_load(ndone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("buffer_inv sc1" ::: "memory");
+    }
+  }
 
   template <int R>
   __device__ void settle(PrefT<R>& pf) {
@@ -975,6 +1007,10 @@ struct EpiConv3 {
         for (int n = 0; n < NTS; ++n) asm volatile("" : "+v"(pf.prev[r][n]));
     }
     asm volatile("" : "+v"(act_h));
+    if (ndone && nrx_tid() < 64) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the poll and the invalidate
+      if (nrx_tid() == 0) *nflag = npoll >= nneed;
+    }
   }
   __device__ void next_hook() const;
 
@@ -1117,7 +1153,7 @@ struct EpiConv3 {
     stamp(6);
     const auto& a = prm->a;
     const int F = a.F, U = a.U;
-    const int lane = threadIdx.x & 63;
+    const int lane = nrx_tid() & 63;
     // ---- new state rows s (C layout, channels >= 56 forced to 0), rounded to S
     Real sv[R][NTS][4];
 #pragma unroll
@@ -1299,6 +1335,18 @@ struct EpiConv3 {
 #endif
 constexpr bool kPrefetchW = NRX_PREFETCH_W != 0;
 
+// Fused forward (k_forward): what an item needs to know about the workgroup's next item and
+// its work queue (nullptr everywhere else).
+template <class P>
+struct FusedNext {
+  const BlockParams<P>* nprm;   // the next item's stage (the sources of its z DMA)
+  const int* ndone;             // its dependency counter (nullptr: no hook)
+  int nneed;
+  int* nflag;                   // LDS word: 1 when the next item's z DMA was issued
+  int* head;                    // this queue's work counter
+  int jnn;                      // thread 0: the item dequeued at the start of this block
+};
+
 // The three layers of a block, in place: conv1 over positions [1, R0-1), conv2 over
 // [2, R0-2), conv3 over [3, R0-3) with the fused epilogue.  P16: conv1's weights are in
 // WB on entry; each layer's global weight loads for the next layer (conv3: + the
@@ -1306,9 +1354,12 @@ constexpr bool kPrefetchW = NRX_PREFETCH_W != 0;
 template <class P, int CINP, int CHP, int TAILM>
 __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, char* WB, int b, int u,
                                             int f_start, int mode, typename P::Real wm, bool first, int nb = -1,
-                                            int nu = 0, int nfs = 0) {
+                                            int nu = 0, int nfs = 0, FusedNext<P>* fn = nullptr) {
   constexpr int R0 = strip_slots<P>();
   const int F = prm.a.F;
+  // fused forward: dequeue the item after next here, past the item's prologue waits (an
+  // older pending atomic would hold every vmcnt wait of wave 0); read at the item's end
+  if (fn && nrx_tid() == 0) fn->jnn = atomicAdd(fn->head, 1);
   {
     SepStage<kHID, kHID> nx;
     if constexpr (P::WLDS && kPrefetchW) nx.load(prm.w[1]);
@@ -1366,9 +1417,16 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
     };
     if constexpr (P::WLDS && readout_tail(TAILM) && kPrefetchW) ld();
     run_layer<P, kHID, kDSP>(X, WB, prm.w[2], 2, kHalo, R0 - kHalo, [&](auto ws) {
-      return EpiConv3<P, decltype(ws), CHP, TAILM>{&prm, X, WB, ws, b, u, f_start, R0 - kHalo, mode, wm, first,
-                                                   (typename P::Real)prm.a.active[(size_t)b * prm.a.U + u],
-                                                   nb, nu, nfs};
+      EpiConv3<P, decltype(ws), CHP, TAILM> e{&prm, X, WB, ws, b, u, f_start, R0 - kHalo, mode, wm, first,
+                                             (typename P::Real)prm.a.active[(size_t)b * prm.a.U + u],
+                                             nb, nu, nfs};
+      if (fn && fn->ndone) {
+        e.nprm = fn->nprm;
+        e.ndone = fn->ndone;
+        e.nneed = fn->nneed;
+        e.nflag = fn->nflag;
+      }
+      return e;
     }, [&]() {
       if constexpr (P::WLDS && TAILM == TAIL_READOUT_WB) {
         // conv3's weights are dead (every wave is past its math): heads into WB
@@ -1429,7 +1487,7 @@ __device__ __forceinline__ NormPre slot_norm_issue(const float* y, int nq) {
   NormPre p;
 #pragma unroll
   for (int k = 0; k < kNormPre; ++k) {
-    const int i = threadIdx.x + 512 * k;
+    const int i = nrx_tid() + 512 * k;
     p.v[k] = yq[i < nq ? i : nq - 1];
   }
   return p;
@@ -1439,14 +1497,14 @@ __device__ __forceinline__ double slot_norm(const NormPre& pre, const float* y, 
   double acc = 0.0;
 #pragma unroll
   for (int k = 0; k < kNormPre; ++k)
-    if (threadIdx.x + 512 * k < nq) acc = sq4(acc, pre.v[k]);
-  for (int i = threadIdx.x + 512 * kNormPre; i < nq; i += 512) {
+    if (nrx_tid() + 512 * k < nq) acc = sq4(acc, pre.v[k]);
+  for (int i = nrx_tid() + 512 * kNormPre; i < nq; i += 512) {
     const floatx4 v = yq[i];
     acc = sq4(acc, v);
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  if ((nrx_tid() & 63) == 0) red[nrx_tid() >> 6] = acc;
   __syncthreads();
   double tot = 0.0;
 #pragma unroll
@@ -1461,15 +1519,15 @@ __global__ __launch_bounds__(1024) void k_norm(const float* __restrict__ y, int 
   __shared__ double red[16];
   const floatx4* yq = reinterpret_cast<const floatx4*>(y) + (size_t)blockIdx.x * nq;
   double acc = 0.0;
-  for (int i = threadIdx.x; i < nq; i += 1024) {
+  for (int i = nrx_tid(); i < nq; i += 1024) {
     const floatx4 v = yq[i];
     acc = sq4(acc, v);
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  if ((nrx_tid() & 63) == 0) red[nrx_tid() >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (nrx_tid() == 0) {
     double tot = 0.0;
     for (int w = 0; w < 16; ++w) tot += red[w];
     const double ms = tot / (double)(4 * nq);
@@ -1486,7 +1544,8 @@ constexpr int kNormFusedMaxQ = 8192;
 
 template <class P, int A2P, int CHP, int TAILM>
 __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem, int b, int u,
-                                          int strip, typename P::Real wm, bool first) {
+                                          int strip, typename P::Real wm, bool first, int nb = -1, int nu = 0,
+                                          int nfs = 0, FusedNext<P>* fn = nullptr) {
   __shared__ double red[8];
   using S = typename P::S;
   using Real = typename P::Real;
@@ -1505,7 +1564,7 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
       // zero once (the z image below occupies the first CINP*32 bytes of each slot; its
       // own t = 14, 15 stores are zeros too, so the two may land in either order)
       constexpr int NQ = kHID * (int)sizeof(S) / 16;
-      for (int idx = threadIdx.x; idx < R0 * 2 * NQ; idx += 512) {
+      for (int idx = nrx_tid(); idx < R0 * 2 * NQ; idx += 512) {
         const int q = idx % NQ, tt = kT + (idx / NQ) % 2, lf = idx / (2 * NQ);
         *reinterpret_cast<intx4*>(X + xoff<P, NQ>(lf, tt, q)) = intx4{0, 0, 0, 0};
       }
@@ -1525,7 +1584,7 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
   if (!prm.norm_pre) npre = slot_norm_issue(yslot, nqs);
   static_assert(R0 * kTP <= 512, "one z row per thread");
   {
-    const int lf = threadIdx.x / kTP, tt = threadIdx.x % kTP;
+    const int lf = nrx_tid() / kTP, tt = nrx_tid() % kTP;
     const int f = f_start + lf;
     const bool ok = lf < R0 && tt < kT && f >= 0 && f < F;
     float yv[A2P], hv[A2P];
@@ -1612,7 +1671,7 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
   stamp(39);
   __syncthreads();
   stamp(1);
-  strip_block<P, CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 1, wm, first);
+  strip_block<P, CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 1, wm, first, nb, nu, nfs, fn);
   stamp(4);
 }
 
@@ -1655,8 +1714,8 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
   constexpr int QS = kDS / P::EPC;   // 7 chunks of a, then 7 of s
   const auto& a = prm.a;
   const int F = a.F, U = a.U;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = nrx_tid() & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(nrx_tid() >> 6);
   const int tq = lane >> 4, qp = lane & 15;
   const S* sp = a.s_in + srow(b, u, 0, 0, U, F);
   const S* ap = a.a + srow(b, U == 2 ? 1 - u : 0, 0, 0, U, F);
@@ -1689,7 +1748,10 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
 
 template <class P, class WS, int CHP, int TAILM>
 __device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook() const {
-  if constexpr (kNextHook || kNextHookRO) zload_dma_u2<P, NRX_DMA_NW>(*prm, X, nb, nu, nfs);
+  if constexpr (kNextHook || kNextHookRO) {
+    if (ndone && !*nflag) return;   // fused forward: the next item's inputs are not complete yet
+    zload_dma_u2<P, NRX_DMA_NW>(nprm ? *nprm : *prm, X, nb, nu, nfs);
+  }
 }
 
 // Rest of an update item whose z image is being filled by LDS-DMA (issued by the caller, or
@@ -1697,7 +1759,8 @@ __device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook() const {
 // block.  (nb, nu, nfs): the next item of a paired workgroup (nb < 0: none).
 template <class P, int CHP, int TAILM>
 __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X, char* WB, int b, int u, int f_start,
-                                             int nb, int nu, int nfs, bool issue_z = false) {
+                                             int nb, int nu, int nfs, bool issue_z = false,
+                                             FusedNext<P>* fn = nullptr) {
   using S = typename P::S;
   constexpr int R0 = strip_slots<P>();
   constexpr int NQ = kUPD_CINP * (int)sizeof(S) / 16;
@@ -1706,7 +1769,7 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
   const int F = a.F;
   SepStage<kUPD_CINP, kHID> w1;
   w1.load(prm.w[0]);
-  const int pe_slot = threadIdx.x / kT, pe_t = threadIdx.x % kT;
+  const int pe_slot = nrx_tid() / kT, pe_t = nrx_tid() % kT;
   const int pe_f = f_start + pe_slot;
   const bool pe_ok = pe_slot < R0 && pe_f >= 0 && pe_f < F;
   const float2 pe_v = *reinterpret_cast<const float2*>(
@@ -1729,7 +1792,7 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
   stamp(27);
   __syncthreads();
   stamp(1);
-  strip_block<P, kUPD_CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 0, 0, false, nb, nu, nfs);
+  strip_block<P, kUPD_CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 0, 0, false, nb, nu, nfs, fn);
   stamp(4);
   if (nb >= 0) stamp(32);   // first item of a pair done
 }
@@ -1808,7 +1871,7 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
     const int uu = inl ? (k < u ? k : k + 1) : u;
     ab[k] = reinterpret_cast<const intx4*>(a.a + srow(b, uu < U ? uu : 0, lo, 0, U, F));
   }
-  const int kk = threadIdx.x % K, r0 = threadIdx.x / K;
+  const int kk = nrx_tid() % K, r0 = nrx_tid() / K;
   const bool lane_on = r0 < RG;
   const int tk = kk / QS, qk = kk % QS;
   intx4 vs[PV], va[PV][kInlineUsers - 1];
@@ -1823,7 +1886,7 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
   }
   // pe chunk (2 values) of z row (slot, t < 14): one row per thread, loaded with the rest
   static_assert(R0 * kT <= 512, "one pe row per thread");
-  const int pe_slot = threadIdx.x / kT, pe_t = threadIdx.x % kT;
+  const int pe_slot = nrx_tid() / kT, pe_t = nrx_tid() % kT;
   const int pe_f = f_start + pe_slot;
   const bool pe_ok = pe_slot < R0 && pe_f >= 0 && pe_f < F;
   // unconditional load from a clamped address (no branch around it: a conditional load
@@ -1836,7 +1899,7 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
   {
     constexpr int ZS = 2 * NQ;                       // chunks per slot (power of 2)
     static_assert((ZS & (ZS - 1)) == 0, "pad block size");
-    for (int idx = threadIdx.x; idx < R0 * ZS; idx += 512)
+    for (int idx = nrx_tid(); idx < R0 * ZS; idx += 512)
       *reinterpret_cast<intx4*>(X + (idx / ZS) * slot_pitch<P>() + (kT * NQ + idx % ZS) * 16) = intx4{0, 0, 0, 0};
   }
   stamp(25);
@@ -1940,7 +2003,7 @@ __global__ __launch_bounds__(256) void k_combine(typename P::S* __restrict__ buf
   using Real = typename P::Real;
   constexpr int QS = kDS / P::EPC;
   const int b = blockIdx.y;
-  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const int idx = blockIdx.x * 256 + nrx_tid();
   if (idx >= F * kT * QS) return;
   const size_t ustride = (size_t)F * kT * kDS;
   S* base = buf + (size_t)b * U * ustride + (size_t)(idx / QS) * kDS + (idx % QS) * P::EPC;
@@ -2007,6 +2070,154 @@ __global__ __launch_bounds__(512) void k_update(BlockParams<P> prm) {
   }
   update_user<P, CHP, TAILM>(prm, smem, b, u, strip);
   stamp(5);
+}
+
+// ================================================================ fused forward (one launch)
+// The whole forward -- StateInit, the num_it state updates and the readouts (neural_rx.py:
+// 544-595) -- as ONE persistent launch, one 512-thread workgroup per CU.  The launch
+// boundaries of the three-launch forward cost every update launch a chip-wide lockstep
+// z-load of its first item (~10 k of ~90 k cycles per CU: all CUs fetch at once) plus the
+// drain/fill of the launch; here a workgroup runs a stream of items and the z image of its
+// next update item is DMA'd during the current item's conv3 epilogue, whatever stage that
+// item belongs to.
+//
+// Work queues.  One queue per XCD (the workgroup reads its XCC id from the hardware), holding
+// the items of the slots b with b % nq == queue in stage-major order: stage 0 (StateInit),
+// then each update; inside a stage slot by slot, (user, strip) within the slot.  A workgroup
+// dequeues with one atomic per item (one item ahead, so the next item is known during the
+// current one's conv3).  An item of stage s >= 1 reads the stage s-1 outputs of its slot
+// (its own and the other user's rows, both strips through the halo), so it waits for the
+// slot's counter done[s-1][b] to reach U * strips.  Items are dequeued in that topological
+// order, and an item only waits for items dequeued before it, i.e. held by workgroups that
+// are running: no deadlock whatever the residency.  The bounded spin (~0.5 s) is a guard
+// only; a timeout sets a sticky error word (nrx_fused_status).
+//
+// Visibility.  Producer and consumer of a hand-off run on the same XCD by construction (the
+// queue is chosen by the XCC id read at run time, not by dispatch order), so the plain
+// 16-byte state stores are in the shared L2 once the storing wave's vmcnt has drained; the
+// producer then signals after a workgroup barrier (one agent-scope atomic add per item).
+// The consumer polls with an sc1 (L1-bypassing) load and invalidates its CU's L1 (buffer_inv
+// sc1) before any load of the handed-off rows: the ping-pong state buffers were read by this
+// CU two stages earlier (MI355X_MICROARCH.md, inter-workgroup visibility).  The counters
+// live in a handle-owned buffer and are reset by the last workgroup to leave.
+struct FusedSync {
+  int head[8];   // per-queue work counters
+  int exits;     // workgroups that left the loop
+  int err;       // sticky: a dependency wait timed out
+  int pad[6];
+  // int done[kFusedMaxStages][B] follows
+};
+constexpr int kFusedMaxStages = 4;   // StateInit + up to 3 updates
+// dynamic LDS of k_forward: the paired-readout layout minus room for the static __shared__
+// words (the slot-norm reduction of StateInit, the queue words); the readout heads must fit
+constexpr int kFusedLds = 160 * 1024 - 256;
+constexpr int kFusedMaxB = 65536;
+constexpr size_t kFusedSyncBytes = sizeof(FusedSync) + (size_t)kFusedMaxStages * kFusedMaxB * sizeof(int);
+
+template <class P>
+struct FusedParams {
+  BlockParams<P> st[kFusedMaxStages];   // 0: StateInit (aggregation tail), 1..nst-1: updates
+  FusedSync* sync;
+  int nst;                              // 1 + num_it
+  int nq;                               // queues (XCDs)
+};
+
+__device__ __forceinline__ int xcc_id() {
+  return (int)__builtin_amdgcn_s_getreg((3 << 11) | 20);   // hwreg(HW_REG_XCC_ID, 0, 4)
+}
+
+// Thread 0 waits for *cnt >= need (bounded), then invalidates this CU's L1 before the
+// workgroup loads the handed-off rows.
+__device__ __forceinline__ void fused_wait(const int* cnt, int need, int* err) {
+  if (nrx_tid() == 0) {
+    int it = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+      __builtin_amdgcn_s_sleep(4);
+      if (++it > (1 << 21)) {
+        __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    asm volatile("buffer_inv sc1" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+template <int A2P, int CHP>
+__global__ __launch_bounds__(512) void k_forward(FusedParams<P16> fp_arg) {
+  using P = P16;
+  // the stage parameters are read through the kernarg segment pointer: indexing the by-value
+  // parameter with the (dynamic) stage made the compiler copy the whole struct to scratch
+  typedef const __attribute__((address_space(4))) FusedParams<P16> KFP;
+  const FusedParams<P16>& fp = *(const FusedParams<P16>*)(KFP*)__builtin_amdgcn_kernarg_segment_ptr();
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int sh[4];   // 0, 1: dequeued items; 2: next z DMA issued; 3: last workgroup
+  constexpr int R0 = strip_slots<P>();
+  char* X = smem;
+  char* WB = smem + R0 * slot_pitch<P>();
+  FusedSync* sy = fp_arg.sync;   // scalars straight from the parameter (keeps it in the kernarg list)
+  int* done = reinterpret_cast<int*>(sy + 1);
+  const int nst = fp_arg.nst, nqs = fp_arg.nq;
+  const auto& a0 = fp.st[0].a;
+  const int B = a0.B, U = a0.U, strips = fp.st[0].strips;
+  const int ips = U * strips;   // items per (stage, slot) = a slot's dependency count
+  const int q = xcc_id() % nqs;
+  const int nbq = (B - q + nqs - 1) / nqs;
+  const int per_stage = nbq * ips, total = nst * per_stage;
+  int* head = &sy->head[q];
+  if (nrx_tid() == 0) {
+    sh[0] = atomicAdd(head, 1);
+    sh[1] = atomicAdd(head, 1);
+  }
+  __syncthreads();
+  int j = sh[0], jn = sh[1];
+  bool have_z = false;   // item j's z image was DMA'd by the previous item's conv3 hook
+  auto decode = [&](int jj, int& s, int& b, int& u, int& strip) {
+    s = jj / per_stage;
+    const int k = jj - s * per_stage;
+    b = q + nqs * (k / ips);
+    u = (k % ips) / strips;
+    strip = k % strips;
+  };
+  while (j < total) {
+    int s, b, u, strip;
+    decode(j, s, b, u, strip);
+    int sn = 0, bn = 0, un = 0, stn = 0;
+    if (jn < total) decode(jn, sn, bn, un, stn);
+    const bool hook = jn < total && sn >= 1;   // the next item's z image can be prefetched
+    FusedNext<P> fn{&fp.st[hook ? sn : 0], hook ? done + (sn - 1) * B + bn : nullptr, ips, &sh[2], head, 0};
+    const int nb = hook ? bn : -1, nfs = stn * P::FO - kHalo;
+    if (s == 0) {
+      const auto& a = fp.st[0].a;
+      float wm = 1.f;
+      if (!a.masking && a.mcs_mask) wm = a.mcs_mask[((size_t)b * U + u) * a.M];
+      init_user<P, A2P, 16, TAIL_AGG>(fp.st[0], smem, b, u, strip, wm, true, nb, un, nfs, &fn);
+    } else {
+      const int fs = strip * P::FO - kHalo;
+      if (!have_z) fused_wait(done + (s - 1) * B + b, ips, &sy->err);
+      if (s == nst - 1)
+        dma_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn);
+      else
+        dma_item_run<P, CHP, TAIL_AGG>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn);
+    }
+    // item done: every wave's stores have reached L2, then one add on the slot's counter
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (nrx_tid() == 0) sh[1] = fn.jnn;
+    __syncthreads();
+    have_z = hook && sh[2] != 0;
+    if (nrx_tid() == 0) __hip_atomic_fetch_add(done + s * B + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    j = jn;
+    jn = sh[1];
+  }
+  // the last workgroup to leave resets the counters for the next forward
+  if (nrx_tid() == 0) sh[3] = atomicAdd(&sy->exits, 1) == (int)(gridDim.x * gridDim.y) - 1;
+  __syncthreads();
+  if (sh[3]) {
+    for (int i = nrx_tid(); i < nst * B; i += 512) done[i] = 0;
+    if (nrx_tid() < 8) sy->head[nrx_tid()] = 0;
+    if (nrx_tid() == 0) sy->exits = 0;
+  }
 }
 
 #include "nrx_rr.inc"
@@ -2356,15 +2567,101 @@ static hipError_t run_rr(const FwdArgs<_Float16, float, _Float16>& args0, const 
   return hipGetLastError();
 }
 
+// NRX_FUSED=0 in the environment (read at every forward) takes the three-launch forward
+// instead of k_forward (A/B and bit-identity tests).
+static bool fused_enabled() {
+  const char* e = getenv("NRX_FUSED");
+  return !e || atoi(e) != 0;
+}
+
+// k_forward covers the throughput tier of the bench-type models: 24-row strips with at least
+// two items per CU, U <= 2 (z images are LDS-DMA copies), one StateInit (no Var-IO mix), one
+// LLR head whose readout fits the paired-readout WB layout, 2A <= 16.
+static bool fused_applicable(const FwdArgs<_Float16, float, _Float16>& a, int num_it, const void* sync) {
+  if (!sync || !fused_enabled()) return false;
+  const long items = (long)a.B * a.U * ((a.F + P16::FO - 1) / P16::FO);
+  return a.U <= 2 && a.num_init == 1 && a.H == 1 && 1 + num_it <= kFusedMaxStages && 2 * a.A <= 16 &&
+         a.B <= kFusedMaxB && items >= 2L * cu_count() && heads_fit_wb(a.bits_max, 16, 2 * a.A) &&
+         30 * kTP * kHID * 2 + kHW2 + 256 * (a.bits_max + 16) <= kFusedLds;
+}
+
+static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, const ModelW<_Float16, float>& W,
+                            int num_it, hipStream_t st, Prof* prof, void* sync) {
+  FusedParams<P16> fp{};
+  fp.sync = reinterpret_cast<FusedSync*>(sync);
+  fp.nst = 1 + num_it;
+  const int cus = cu_count();
+  fp.nq = cus / 32 < 1 ? 1 : (cus / 32 > 8 ? 8 : cus / 32);   // MI355X: 8 XCDs x 32 CUs
+  const int nq = args.F * kT * 2 * args.A / 4;
+  const bool norm_pre = nq > kNormFusedMaxQ;
+  auto B_ = [&](int k) { if (prof) prof->begin(k, st); };
+  auto E_ = [&](int k) { if (prof) prof->end(k, st); };
+  if (norm_pre) {
+    B_(K_NORM);
+    k_norm<<<args.B, 1024, 0, st>>>(args.y, nq, args.norm);
+    E_(K_NORM);
+  }
+  FwdArgs<_Float16, float, _Float16> a = args;
+  for (int s = 0; s < fp.nst; ++s) {
+    BlockParams<P16>& bp = fp.st[s];
+    bp.inline_combine = 1;
+    bp.pair = 0;
+    bp.order_rev = 0;
+    bp.norm_pre = norm_pre;
+    bp.strips = (args.F + P16::FO - 1) / P16::FO;
+    bp.m = 0;
+    for (int h = 0; h < args.H; ++h) {
+      bp.llr[h][0] = W.llr[h][0];
+      bp.llr[h][1] = W.llr[h][1];
+    }
+    bp.chest[0] = W.chest[0];
+    bp.chest[1] = W.chest[1];
+    if (s == 0) {
+      for (int l = 0; l < 3; ++l) bp.w[l] = W.init[0][l];
+      bp.tail = TAIL_AGG;
+      bp.agg[0] = W.agg[0][0];
+      bp.agg[1] = W.agg[0][1];
+    } else {
+      std::swap(a.s_in, a.s_out);
+      std::swap(a.a, a.a_out);
+      const int i = s - 1;
+      for (int l = 0; l < 3; ++l) bp.w[l] = W.upd[i][l];
+      const bool last = i == num_it - 1;
+      bp.tail = last ? TAIL_READOUT_WB : TAIL_AGG;
+      if (!last) {
+        bp.agg[0] = W.agg[i + 1][0];
+        bp.agg[1] = W.agg[i + 1][1];
+      }
+    }
+    bp.a = a;
+  }
+  constexpr int L = kFusedLds;
+  B_(K_FUSED);
+  if (2 * args.A <= 8) k_forward<8, 16><<<cus, 512, L, st>>>(fp);
+  else k_forward<16, 16><<<cus, 512, L, st>>>(fp);
+  E_(K_FUSED);
+  return hipGetLastError();
+}
+
 hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args,
                               const ModelW<_Float16, float>& W, const RrImages* rr, int num_it, hipStream_t st,
-                              Prof* prof) {
+                              Prof* prof, void* fused_sync) {
   if (NRX_SMALL_STRIPS != 0) {
     if (small_strips_fit<P16S>(args)) return Launch<P16S>::run(args, W, num_it, st, prof);
     if (small_strips_fit<P16M>(args)) return Launch<P16M>::run(args, W, num_it, st, prof);
   }
   if (rr_applicable(args, rr)) return run_rr(args, W, *rr, num_it, st, prof);
+  if (fused_applicable(args, num_it, fused_sync)) return run_fused(args, W, num_it, st, prof, fused_sync);
   return Launch<P16>::run(args, W, num_it, st, prof);
+}
+
+size_t fused_sync_bytes() { return kFusedSyncBytes; }
+
+// sticky error word of the fused forward's dependency waits (blocking read; clear: reset)
+hipError_t fused_sync_status(void* sync, int* err, bool reset) {
+  hipError_t e = hipMemcpy(err, &reinterpret_cast<FusedSync*>(sync)->err, sizeof(int), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && reset) e = hipMemset(&reinterpret_cast<FusedSync*>(sync)->err, 0, sizeof(int));
+  return e;
 }
 
 hipError_t launch_forward_f64(const FwdArgs<double, double, float>& args,
@@ -2388,6 +2685,10 @@ hipError_t setup_kernels() {
     }
   }
   hipError_t e2 = Launch<P64>::setup();
+  for (const void* f : {(const void*)k_forward<8, 16>, (const void*)k_forward<16, 16>}) {
+    hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kFusedLds);
+    if (r != hipSuccess && e2 == hipSuccess) e2 = r;
+  }
   return e != hipSuccess ? e : (e1 != hipSuccess ? e1 : e2);
 }
 

@@ -34,7 +34,8 @@ def launch_flops_per_re_user(spec: ModelSpec, num_it: int) -> dict:
     k = kernel_flops_per_re_user(spec)
     return {"norm": 0,
             "state_init": k["state_init"] + k["aggregate"],
-            "state_update": k["state_update"] + ((num_it - 1) * k["aggregate"] + k["readout"]) / num_it}
+            "state_update": k["state_update"] + ((num_it - 1) * k["aggregate"] + k["readout"]) / num_it,
+            "forward": forward_flops_per_re_user(spec, num_it)}
 
 
 def update_launch_bytes_per_re_user(spec: ModelSpec, num_it: int, elem: int = 2) -> float:
@@ -45,6 +46,36 @@ def update_launch_bytes_per_re_user(spec: ModelSpec, num_it: int, elem: int = 2)
     mid = 4 * st
     last = 2 * st + 4 * (spec.bits_max * spec.num_llr_heads + 2 * spec.num_rx_ant)
     return ((num_it - 1) * mid + last) / num_it
+
+
+def init_launch_bytes_per_re_user(spec: ModelSpec, num_users: int, elem: int = 2) -> float:
+    """Algorithmic HBM bytes per RE-user of the StateInit launch: y (f32, shared by the
+    slot's users) and h_hat (f32) in, s and act*sp out in storage precision."""
+    a2 = 2 * spec.num_rx_ant
+    return a2 * 4 / num_users + (a2 * 4 if spec.use_h_hat else 0) + 2 * spec.d_s * elem
+
+
+def forward_bytes_per_re_user(spec: ModelSpec, num_it: int, num_users: int, elem: int = 2) -> float:
+    """Algorithmic HBM bytes per RE-user of the one-launch forward (k_forward): the same
+    hand-offs as the three-launch schedule -- StateInit's, then every update's."""
+    return init_launch_bytes_per_re_user(spec, num_users, elem) + num_it * update_launch_bytes_per_re_user(
+        spec, num_it, elem)
+
+
+def forward_split_per_re_user(spec: ModelSpec, num_it: int) -> dict:
+    """The whole forward's algorithmic FLOPs split by pipe (depthwise taps on the VALU)."""
+    u1, u2 = spec.init_units
+    v1, v2 = spec.state_units
+    dw = 2 * 9 * (spec.num_init * (spec.init_in_ch + u1 + u2) + num_it * (spec.update_in_ch + v1 + v2))
+    total = forward_flops_per_re_user(spec, num_it)
+    return {"depthwise_valu": dw, "dense_mfma": total - dw, "total": total}
+
+
+def forward_mixed_bound_tflops(spec: ModelSpec, num_it: int, mfma_tflops: float = 2500.0,
+                               valu_tflops: float = 157.3) -> float:
+    """mixed_bound_tflops for the whole forward (the one-launch kernel)."""
+    s = forward_split_per_re_user(spec, num_it)
+    return s["total"] / (s["dense_mfma"] / mfma_tflops + s["depthwise_valu"] / valu_tflops)
 
 
 def forward_flops_per_re_user(spec: ModelSpec, num_it: int) -> int:

@@ -91,6 +91,12 @@ class CGNNEngine:
     def profile(self, enable: bool = True):
         _lib.check(self._lib.nrx_profile_enable(self._h, int(enable)))
 
+    def fused_status(self, reset: bool = False) -> int:
+        """Sticky error word of the one-launch forward (1: a dependency wait timed out)."""
+        err = ctypes.c_int32()
+        _lib.check(self._lib.nrx_fused_status(self._h, ctypes.byref(err), int(reset)))
+        return err.value
+
     def profile_read(self):
         """{kernel: (launches, total_ms)} since the last profile(True)."""
         out = {}
