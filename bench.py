@@ -127,6 +127,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    eng.fused_status(reset=True)
     ev_t0, ev_t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev_t0.record()
@@ -139,6 +140,7 @@ def main():
     elapsed = time.perf_counter() - t0
     # the launch stream's own clock over the same timed region (no per-launch markers)
     stream_step_ms = ev_t0.elapsed_time(ev_t1) / args.steps
+    fused_st = eng.fused_status(full=True)   # one-launch forward: prefetch misses in the timed region
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -230,6 +232,12 @@ def main():
                 "frac_of_mixed_bound": round(achieved / mixed, 4) if mixed else None,
                 "mixed_bound_note": mixed_note,
                 "traffic_source": pmc_src}
+    if fused:
+        upd_items = args.steps * num_it * U * B * ((F + 23) // 24)
+        roofline["fused_queue"] = {"update_items_waited": fused_st["waited"], "update_items": upd_items,
+                                   "polls": fused_st["polls"], "error": fused_st["error"],
+                                   "note": "update items whose inputs were not complete when the previous item "
+                                           "polled (z image loaded after a wait, not during that item's epilogue)"}
 
     # ---- batch-1 per-slot latency (hipGraph replay; device-only and H2D+compute+D2H)
     latency = None

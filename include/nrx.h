@@ -288,12 +288,14 @@ int nrx_profile_read(nrx_handle* h, int32_t kernel, int64_t* launches, double* t
 
 /* The throughput tier of nrx_forward (f16, 24-row strips, >= 2 items per CU, U <= 2, one
  * StateInit, one LLR head) runs the whole forward as ONE persistent launch whose items wait
- * on per-(stage, slot) counters in a handle-owned buffer.  Its waits are bounded; *error is
- * set to 1 (sticky) if one ever timed out (results of that forward are then invalid).
- * Blocking; reset != 0 clears the word.  Forwards on one handle must not run concurrently
- * on several streams (the counters are per handle).  NRX_FUSED=0 in the environment takes
- * the three-launch path instead. */
-int nrx_fused_status(nrx_handle* h, int32_t* error, int32_t reset);
+ * on per-(stage, slot) counters in a handle-owned buffer.  status[3] since the last reset:
+ * [0] error bits (1: a bounded dependency wait timed out, 2: items left undone -- the
+ * results of that forward are invalid), [1] update items whose inputs were not complete when
+ * the previous item polled for them (their z image loaded after a wait instead of during
+ * that item's epilogue), [2] the polls those waits took.  Blocking; reset != 0 clears them.
+ * Forwards on one handle must not run concurrently on several streams (the counters are
+ * per handle).  NRX_FUSED=0 in the environment takes the three-launch path instead. */
+int nrx_fused_status(nrx_handle* h, int32_t* status, int32_t reset);
 
 const char* nrx_last_error(void);
 int32_t nrx_api_version(void);

@@ -217,7 +217,7 @@ def load(path: str = LIB_PATH):
     lib.nrx_profile_enable.restype = c.c_int
     lib.nrx_profile_read.argtypes = [c.c_void_p, c.c_int32, P(c.c_int64), P(c.c_double)]
     lib.nrx_profile_read.restype = c.c_int
-    lib.nrx_fused_status.argtypes = [c.c_void_p, P(c.c_int32), c.c_int32]
+    lib.nrx_fused_status.argtypes = [c.c_void_p, c.c_void_p, c.c_int32]
     lib.nrx_fused_status.restype = c.c_int
     lib.nrx_aerial_workspace_size.argtypes = [c.c_void_p, P(nrx_aerial_io), P(c.c_size_t)]
     lib.nrx_aerial_workspace_size.restype = c.c_int

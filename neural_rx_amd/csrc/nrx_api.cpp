@@ -22,7 +22,7 @@ namespace nrx {
 hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args, const ModelW<_Float16, float>& W,
                               const RrImages* rr, int num_it, hipStream_t st, Prof* prof, void* fused_sync);
 size_t fused_sync_bytes();
-hipError_t fused_sync_status(void* sync, int* err, bool reset);
+hipError_t fused_sync_status(void* sync, int* st, bool reset);
 hipError_t launch_forward_f64(const FwdArgs<double, double, float>& args,
                               const ModelW<double, double>& W, int num_it, hipStream_t st,
                               Prof* prof);
@@ -827,12 +827,12 @@ int nrx_profile_enable(nrx_handle* h, int32_t enable) {
   return NRX_OK;
 }
 
-int nrx_fused_status(nrx_handle* h, int32_t* error, int32_t reset) {
-  if (!h || !error) return fail(NRX_ERR_INVALID_ARG, "null argument");
-  int err = 0;
-  hipError_t e = fused_sync_status(h->fused_sync, &err, reset != 0);
+int nrx_fused_status(nrx_handle* h, int32_t* status, int32_t reset) {
+  if (!h || !status) return fail(NRX_ERR_INVALID_ARG, "null argument");
+  int st[3] = {0, 0, 0};
+  hipError_t e = fused_sync_status(h->fused_sync, st, reset != 0);
   if (e != hipSuccess) return hip_fail(e, "fused status");
-  *error = err;
+  for (int i = 0; i < 3; ++i) status[i] = st[i];
   return NRX_OK;
 }
 

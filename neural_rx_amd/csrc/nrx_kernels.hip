@@ -56,10 +56,26 @@ __device__ unsigned long long g_nrx_stamps[4096][64];
 // set by the host for the k_update launch to record; __constant__ so that the flag is a
 // scalar (SMEM) load and a stamp does not wait for the wave's outstanding vector loads
 __constant__ int g_nrx_stamp_on;
+// one-launch forward (g_nrx_stamp_on == 100): per item i < 8 of a workgroup, slots
+// g_nrx_rr_stamps[wg][8 i + m]: 0 item start, 1 conv1 start, 2 conv1 end, 3 conv2 end,
+// 4 conv3 epilogue start, 5 item body done, 6 signalled, 7 = stage + 1 (not a time)
+__device__ unsigned long long g_nrx_rr_stamps[4096][64];
+__device__ int g_fstamp_item[4096];
+__device__ __forceinline__ void fstamp(int m) {
+  if (threadIdx.x == 0 && g_nrx_stamp_on == 100) {
+    const int wg = blockIdx.x, it = g_fstamp_item[wg];
+    if (wg < 4096 && it < 8) g_nrx_rr_stamps[wg][8 * it + m] = __builtin_amdgcn_s_memtime();
+  }
+}
 __device__ __forceinline__ void stamp(int k) {
   if (threadIdx.x == 0 && g_nrx_stamp_on) {
     const int wg = blockIdx.x;
-    if (wg < 4096) g_nrx_stamps[wg][k] = __builtin_amdgcn_s_memtime();
+    if (g_nrx_stamp_on == 100) {
+      const int m = k == 1 ? 1 : k == 2 ? 2 : k == 3 ? 3 : k == 6 ? 4 : -1;
+      if (m >= 0) fstamp(m);
+    } else if (wg < 4096) {
+      g_nrx_stamps[wg][k] = __builtin_amdgcn_s_memtime();
+    }
   }
 }
 // per-wave stamp k + wave (lane 0 of every wave), k in {40, 48, 56}
@@ -71,7 +87,6 @@ __device__ __forceinline__ void stamp_w(int k) {
 }
 // register-resident kernels (own array): phase ph (0..31) of the workgroup's item ks == 1,
 // for wave 0 (R = 3, no DMA duty) and wave 4 (R = 2, DMA issuer) of the same SIMD
-__device__ unsigned long long g_nrx_rr_stamps[4096][64];
 __device__ __forceinline__ void rr_stamp(int ks, int ph) {
   if (ks == 1 && (threadIdx.x & 255) == 0 && g_nrx_stamp_on) {
     const int wg = blockIdx.x;
@@ -79,6 +94,7 @@ __device__ __forceinline__ void rr_stamp(int ks, int ph) {
   }
 }
 #else
+__device__ __forceinline__ void fstamp(int) {}
 __device__ __forceinline__ void stamp(int) {}
 __device__ __forceinline__ void stamp_w(int) {}
 __device__ __forceinline__ void rr_stamp(int, int) {}
@@ -96,9 +112,14 @@ typedef int intx8 __attribute__((ext_vector_type(8)));
 // the item code inside a loop, and LLVM's LICM hoisted every thread-index-derived address of
 // every item body out of it -- ~70 values live across the whole loop, spilled to scratch and
 // reloaded in the conv loops.  An opaque id per use keeps each derivation where it is used.
+#ifndef NRX_OPAQUE_TID
+#define NRX_OPAQUE_TID 2
+#endif
 __device__ __forceinline__ unsigned nrx_tid() {
   unsigned t = threadIdx.x;
-  asm volatile("" : "+v"(t));
+  if (NRX_OPAQUE_TID == 1) asm volatile("" : "+v"(t));
+  if (NRX_OPAQUE_TID == 2) asm("" : "+v"(t));   // CSE-able, not speculatable: not hoisted
+  if (NRX_OPAQUE_TID) __builtin_assume(t < 1024);   // the range the compiler loses
   return t;
 }
 
@@ -542,7 +563,7 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
   typename E::template PrefT<R> pf;
   stamp(8 + 5 * in_off);
   if (act) epi.template prefetch<R>(pf, p0, t, g);   // epilogue global loads, in flight during the math
-  if constexpr (E::kNextHook || E::kNextHookRO) epi.poll();
+  if constexpr (E::kNextHook || E::kNextHookRO) epi.stage_next();
   if (act) {
     if constexpr (NRX_ABLATE & 1) {
 #pragma unroll
@@ -941,6 +962,85 @@ __device__ __forceinline__ int head_w2(int h) { return head_w1(h) + 16 * 1024; }
 __device__ __forceinline__ int head_b1(int h) { return head_w1(h) + kHeadSlot; }
 __device__ __forceinline__ int head_b2(int h) { return head_b1(h) + 512; }
 
+#ifndef NRX_ZSTAGE
+#define NRX_ZSTAGE 0   // 1: register-staged next-item z image (measured slower)
+#endif
+
+// The z image [a | s | pe] of a workgroup's NEXT update item (U <= 2: a = the other user's
+// act*sp plane, or 0), staged through registers.  The loads are issued at the start of the
+// current item's conv3 layer -- 64 output channels, so ~60 VGPRs are free there -- and their
+// latency hides behind the conv3 math; once every wave is past its conv3 reads the values are
+// written into the strip image (commit), before the epilogue.  The LDS-DMA it replaces issued
+// 123 KB after the conv3 math and held the issuing waves ~6.5 k cycles (profiles/r02/
+// stamps_pair_dma.txt).  Per 16-row slot of a (b, u) plane the in-grid rows are contiguous
+// (14 symbols x 7 chunks), so thread c of the concatenated a | s chunk range loads chunk c:
+// coalesced 16-byte loads, 12 per thread.  Out-of-grid rows and the missing plane are zeros;
+// the pad symbols t = 14, 15 of the strip image are zero already (set at the workgroup's first
+// item, never written by the conv layers) and are not touched.
+template <class P>
+struct ZStage {
+  using S = typename P::S;
+  static constexpr int R0 = strip_slots<P>();
+  static constexpr int QS = kDS / 8;                 // chunks of a plane row per symbol (7)
+  static constexpr int ROWC = kT * QS;               // chunks per grid row (98)
+  static constexpr int PLANE = R0 * ROWC;            // chunks of one plane over the strip
+  static constexpr int NL = (2 * PLANE + 511) / 512;
+  static constexpr int NPE = R0 * kT;                // (slot, t < 14) pairs: pe + zero chunks
+  static_assert(NPE <= 512, "one pe chunk per thread");
+  intx4 v[NL];
+  float2 pe;
+  int f_start, F, U;
+  // raw loads only: every mask is applied in commit -- a select here made the compiler wait
+  // for the loads right at the start of the conv3 math
+  __device__ void issue(const BlockParams<P>& np, int b, int u, int fs) {
+    const auto& a = np.a;
+    f_start = fs;
+    F = a.F;
+    U = a.U;
+    const int tid = nrx_tid();
+    const S* sp = a.s_in + srow(b, u, 0, 0, U, F);
+    const S* ap = U == 2 ? a.a + srow(b, 1 - u, 0, 0, U, F) : sp;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int c = tid + 512 * i;
+      const int pl = c >= PLANE;
+      const int k = c - pl * PLANE;
+      const int f = f_start + k / ROWC;
+      const bool ok = c < 2 * PLANE && f >= 0 && f < F;
+      // unconditional load from a clamped address (no branch around it)
+      const unsigned off = ok ? (unsigned)(f * ROWC + k % ROWC) : 0u;
+      v[i] = reinterpret_cast<const intx4*>(pl ? sp : ap)[off];
+    }
+    const int slot = tid / kT, t = tid % kT, f = f_start + slot;
+    const bool ok = tid < NPE && f >= 0 && f < F;
+    pe = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + (ok ? f : 0)) * kT + (ok ? t : 0)) * 2);
+  }
+  __device__ void commit(char* X) const {
+    const int tid = nrx_tid();
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int c = tid + 512 * i;
+      if (c < 2 * PLANE) {
+        const int pl = c >= PLANE;
+        const int k = c - pl * PLANE;
+        const int slot = k / ROWC, t = (k % ROWC) / QS, q = k % QS + pl * QS;
+        const int f = f_start + slot;
+        const bool ok = f >= 0 && f < F && (pl || U == 2);
+        *reinterpret_cast<intx4*>(X + xoff<P, 16>(slot, t, q)) = ok ? v[i] : intx4{0, 0, 0, 0};
+      }
+    }
+    if (tid < NPE) {
+      const int slot = tid / kT, t = tid % kT, f = f_start + slot;
+      const bool ok = f >= 0 && f < F;
+      S pe2[P::EPC] = {};
+      pe2[0] = ok ? (S)pe.x : (S)0;
+      pe2[1] = ok ? (S)pe.y : (S)0;
+      *reinterpret_cast<intx4*>(X + xoff<P, 16>(slot, t, 2 * QS)) = *reinterpret_cast<const intx4*>(pe2);
+      *reinterpret_cast<intx4*>(X + xoff<P, 16>(slot, t, 2 * QS + 1)) = intx4{0, 0, 0, 0};
+    }
+  }
+};
+
 #ifndef NRX_RO_STRAIGHT
 #define NRX_RO_STRAIGHT 1
 #endif
@@ -977,24 +1077,19 @@ struct EpiConv3 {
   int nb, nu, nfs;        // paired k_update: next item (nb < 0: none)
   int pos_lo = 0;         // first strip position with an output row (RR blocks: kHalo)
   // fused forward (k_forward): the next item belongs to stage nprm and may start only once
-  // its dependency counter ndone has reached nneed.  The counter is polled at the start of
-  // the conv3 layer (poll), its value is read after the math (settle), and the next z DMA is
-  // issued only when it was complete (nflag, LDS).  ndone == nullptr: no dependency (paired
-  // items of one launch).
+  // its dependency counter has reached its target; strip_block polls the counter at the start
+  // of conv2 and leaves the verdict in nflag (LDS) for conv3.  ndone == nullptr: no
+  // dependency (paired items of one launch).
   const BlockParams<P>* nprm = nullptr;
   const int* ndone = nullptr;
-  int nneed = 0;
   int* nflag = nullptr;
-  int npoll = 0;
+  ZStage<P> zs;   // the next item's z image in flight (NRX_ZSTAGE)
 
-  // wave 0 lane 0: the dependency counter of the next item (sc1 load: L2-served), then an
-  // agent-scope L1 invalidate, so that no line of the next item's inputs this CU read in an
-  // earlier stage (ping-pong buffers) is still valid when its z DMA and skip rows load them.
-  // Both complete asynchronously behind the conv3 math; settle waits for them.
-  __device__ void poll() {
-    if (ndone && nrx_tid() == 0) {
-      npoll = __hip_atomic_load(ndone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("buffer_inv sc1" ::: "memory");
+  __device__ bool next_ready() const { return nb >= 0 && (!ndone || *nflag); }
+  // conv3 start, every thread: the next item's z loads (their latency hides behind the math)
+  __device__ void stage_next() {
+    if constexpr (NRX_ZSTAGE != 0 && (kNextHook || kNextHookRO)) {
+      if (next_ready()) zs.issue(nprm ? *nprm : *prm, nb, nu, nfs);
     }
   }
 
@@ -1007,12 +1102,8 @@ struct EpiConv3 {
         for (int n = 0; n < NTS; ++n) asm volatile("" : "+v"(pf.prev[r][n]));
     }
     asm volatile("" : "+v"(act_h));
-    if (ndone && nrx_tid() < 64) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the poll and the invalidate
-      if (nrx_tid() == 0) *nflag = npoll >= nneed;
-    }
   }
-  __device__ void next_hook() const;
+  __device__ void next_hook();
 
   __device__ bool row_ok(int p, int t) const {
     return p >= pos_lo && p < pos_hi && f_start + p < prm->a.F && t < kT;
@@ -1387,9 +1478,23 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
       }
     };
     if constexpr (P::WLDS && kPrefetchW) ld();
+    // fused forward: thread 0 polls the next item's dependency counter (an sc1 load, L2-
+    // served) and invalidates this CU's L1 -- no line of the next item's inputs this CU read
+    // in an earlier stage (ping-pong buffers) may survive into its loads; both complete
+    // behind the conv2 math.  The verdict goes to nflag for conv3's stage_next / next_hook.
+    int pv = 0;
+    const bool poll = fn && fn->ndone && nrx_tid() == 0;
+    if (poll) {
+      pv = __hip_atomic_load(fn->ndone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("buffer_inv sc1" ::: "memory");
+    }
     run_layer<P, kHID, kHID>(X, WB, prm.w[1], 1, 2, R0 - 2, [&](auto ws) {
       return EpiInPlace<P, kHID, decltype(ws)>{X, 1, R0 - 2, f_start, F, ws};
     }, [&]() {
+      if (poll) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the poll and the invalidate
+        *fn->nflag = pv >= fn->nneed;
+      }
       if constexpr (P::WLDS) {
         if constexpr (!kPrefetchW) ld();
         nx.store(WB);
@@ -1423,7 +1528,6 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
       if (fn && fn->ndone) {
         e.nprm = fn->nprm;
         e.ndone = fn->ndone;
-        e.nneed = fn->nneed;
         e.nflag = fn->nflag;
       }
       return e;
@@ -1747,10 +1851,11 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
 }
 
 template <class P, class WS, int CHP, int TAILM>
-__device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook() const {
+__device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook() {
   if constexpr (kNextHook || kNextHookRO) {
-    if (ndone && !*nflag) return;   // fused forward: the next item's inputs are not complete yet
-    zload_dma_u2<P, NRX_DMA_NW>(nprm ? *nprm : *prm, X, nb, nu, nfs);
+    if (!next_ready()) return;   // fused forward: the next item's inputs were not complete
+    if constexpr (NRX_ZSTAGE != 0) zs.commit(X);
+    else zload_dma_u2<P, NRX_DMA_NW>(nprm ? *nprm : *prm, X, nb, nu, nfs);
   }
 }
 
@@ -1769,11 +1874,14 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
   const int F = a.F;
   SepStage<kUPD_CINP, kHID> w1;
   w1.load(prm.w[0]);
+  // a z image staged by the previous item (ZStage) holds the pe chunk already
+  const bool staged = !issue_z && NRX_ZSTAGE != 0;
   const int pe_slot = nrx_tid() / kT, pe_t = nrx_tid() % kT;
   const int pe_f = f_start + pe_slot;
   const bool pe_ok = pe_slot < R0 && pe_f >= 0 && pe_f < F;
-  const float2 pe_v = *reinterpret_cast<const float2*>(
-      a.pe + (((size_t)u * F + (pe_ok ? pe_f : 0)) * kT + (pe_ok ? pe_t : 0)) * 2);
+  float2 pe_v = float2{0.f, 0.f};
+  if (!staged)
+    pe_v = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + (pe_ok ? pe_f : 0)) * kT + (pe_ok ? pe_t : 0)) * 2);
   // first item of a workgroup: its z DMA goes out behind the conv1-weight and pe loads, so
   // their latency hides under the DMA instead of following it
   if (issue_z) zload_dma_u2<P>(prm, X, b, u, f_start);
@@ -1782,7 +1890,7 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();   // every wave's DMA has landed (and a previous item's epilogue is done)
   stamp(26);
-  if (pe_slot < R0) {
+  if (!staged && pe_slot < R0) {
     S pe2[P::EPC] = {};
     pe2[0] = pe_ok ? (S)pe_v.x : (S)0;
     pe2[1] = pe_ok ? (S)pe_v.y : (S)0;
@@ -2104,7 +2212,9 @@ struct FusedSync {
   int head[8];   // per-queue work counters
   int exits;     // workgroups that left the loop
   int err;       // sticky: a dependency wait timed out
-  int pad[6];
+  int waited;    // update items whose z image was not prefetched (dependency not met in time)
+  int spins;     // dependency-wait polls of those items
+  int pad[4];
   // int done[kFusedMaxStages][B] follows
 };
 constexpr int kFusedMaxStages = 4;   // StateInit + up to 3 updates
@@ -2128,16 +2238,18 @@ __device__ __forceinline__ int xcc_id() {
 
 // Thread 0 waits for *cnt >= need (bounded), then invalidates this CU's L1 before the
 // workgroup loads the handed-off rows.
-__device__ __forceinline__ void fused_wait(const int* cnt, int need, int* err) {
+__device__ __forceinline__ void fused_wait(const int* cnt, int need, FusedSync* sy) {
   if (nrx_tid() == 0) {
     int it = 0;
     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
       __builtin_amdgcn_s_sleep(4);
       if (++it > (1 << 21)) {
-        __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_or(&sy->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
+    __hip_atomic_fetch_add(&sy->waited, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (it) __hip_atomic_fetch_add(&sy->spins, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("buffer_inv sc1" ::: "memory");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -2180,9 +2292,20 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P16> fp_arg) {
     u = (k % ips) / strips;
     strip = k % strips;
   };
+#ifdef NRX_STAMPS
+  int n_item = 0;
+#endif
   while (j < total) {
     int s, b, u, strip;
     decode(j, s, b, u, strip);
+#ifdef NRX_STAMPS
+    if (nrx_tid() == 0 && blockIdx.x < 4096) {
+      g_fstamp_item[blockIdx.x] = n_item;
+      if (n_item < 8 && g_nrx_stamp_on == 100) g_nrx_rr_stamps[blockIdx.x][8 * n_item + 7] = s + 1;
+    }
+    ++n_item;
+    fstamp(0);
+#endif
     int sn = 0, bn = 0, un = 0, stn = 0;
     if (jn < total) decode(jn, sn, bn, un, stn);
     const bool hook = jn < total && sn >= 1;   // the next item's z image can be prefetched
@@ -2195,25 +2318,36 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P16> fp_arg) {
       init_user<P, A2P, 16, TAIL_AGG>(fp.st[0], smem, b, u, strip, wm, true, nb, un, nfs, &fn);
     } else {
       const int fs = strip * P::FO - kHalo;
-      if (!have_z) fused_wait(done + (s - 1) * B + b, ips, &sy->err);
+      if (!have_z) fused_wait(done + (s - 1) * B + b, ips, sy);
       if (s == nst - 1)
         dma_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn);
       else
         dma_item_run<P, CHP, TAIL_AGG>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn);
     }
+    fstamp(5);
     // item done: every wave's stores have reached L2, then one add on the slot's counter
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (nrx_tid() == 0) sh[1] = fn.jnn;
     __syncthreads();
     have_z = hook && sh[2] != 0;
+    fstamp(6);
     if (nrx_tid() == 0) __hip_atomic_fetch_add(done + s * B + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     j = jn;
     jn = sh[1];
   }
   // the last workgroup to leave resets the counters for the next forward
-  if (nrx_tid() == 0) sh[3] = atomicAdd(&sy->exits, 1) == (int)(gridDim.x * gridDim.y) - 1;
+  if (nrx_tid() == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's last counter add has landed
+    sh[3] = atomicAdd(&sy->exits, 1) == (int)(gridDim.x * gridDim.y) - 1;
+  }
   __syncthreads();
   if (sh[3]) {
+    // every item ran (a queue whose XCD never received a workgroup would leave its slots
+    // undone: error word 2), then the reset
+    for (int i = nrx_tid(); i < nst * B; i += 512)
+      if (__hip_atomic_load(done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ips)
+        __hip_atomic_fetch_or(&sy->err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
     for (int i = nrx_tid(); i < nst * B; i += 512) done[i] = 0;
     if (nrx_tid() < 8) sy->head[nrx_tid()] = 0;
     if (nrx_tid() == 0) sy->exits = 0;
@@ -2636,6 +2770,13 @@ static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, cons
     bp.a = a;
   }
   constexpr int L = kFusedLds;
+#ifdef NRX_STAMPS
+  {
+    const int on = getenv("NRX_STAMP_FUSED") ? 100 : 0;
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_nrx_stamp_on), &on, sizeof(int), 0, hipMemcpyHostToDevice, st);
+    (void)hipStreamSynchronize(st);
+  }
+#endif
   B_(K_FUSED);
   if (2 * args.A <= 8) k_forward<8, 16><<<cus, 512, L, st>>>(fp);
   else k_forward<16, 16><<<cus, 512, L, st>>>(fp);
@@ -2657,10 +2798,12 @@ hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args,
 
 size_t fused_sync_bytes() { return kFusedSyncBytes; }
 
-// sticky error word of the fused forward's dependency waits (blocking read; clear: reset)
-hipError_t fused_sync_status(void* sync, int* err, bool reset) {
-  hipError_t e = hipMemcpy(err, &reinterpret_cast<FusedSync*>(sync)->err, sizeof(int), hipMemcpyDeviceToHost);
-  if (e == hipSuccess && reset) e = hipMemset(&reinterpret_cast<FusedSync*>(sync)->err, 0, sizeof(int));
+// {error word, items that waited, polls} of the fused forward since the last reset
+// (blocking read; reset clears the three words)
+hipError_t fused_sync_status(void* sync, int* st, bool reset) {
+  FusedSync* sy = reinterpret_cast<FusedSync*>(sync);
+  hipError_t e = hipMemcpy(st, &sy->err, 3 * sizeof(int), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && reset) e = hipMemset(&sy->err, 0, 3 * sizeof(int));
   return e;
 }
 

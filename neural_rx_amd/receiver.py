@@ -91,11 +91,15 @@ class CGNNEngine:
     def profile(self, enable: bool = True):
         _lib.check(self._lib.nrx_profile_enable(self._h, int(enable)))
 
-    def fused_status(self, reset: bool = False) -> int:
-        """Sticky error word of the one-launch forward (1: a dependency wait timed out)."""
-        err = ctypes.c_int32()
-        _lib.check(self._lib.nrx_fused_status(self._h, ctypes.byref(err), int(reset)))
-        return err.value
+    def fused_status(self, reset: bool = False, full: bool = False):
+        """One-launch forward counters since the last reset: the sticky error bits (1: a
+        dependency wait timed out, 2: items left undone), or with ``full`` the dict
+        {error, waited, polls} (update items that could not be prefetched, and their polls)."""
+        st = (ctypes.c_int32 * 3)()
+        _lib.check(self._lib.nrx_fused_status(self._h, st, int(reset)))
+        if full:
+            return {"error": st[0], "waited": st[1], "polls": st[2]}
+        return st[0]
 
     def profile_read(self):
         """{kernel: (launches, total_ms)} since the last profile(True)."""
