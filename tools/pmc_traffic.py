@@ -48,8 +48,18 @@ def main(fdir, wdir, key, source=None, num_it=2):
         rec["source"] = source
     if upd_mid and upd_last:
         rec["k_update_bytes_per_launch"] = round(((num_it - 1) * upd_mid[0] + upd_last[0]) / num_it)
+    # the one-launch forward (k_forward<A2P, CHP>): one instantiation per model shape
+    fwd = [v["bytes"] for k, v in out.items() if k.startswith("nrx::k_forward")]
+    if fwd:
+        rec["k_forward_bytes_per_launch"] = round(fwd[0])
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     data = json.load(open(path)) if os.path.exists(path) else {}
+    # keep the fields of an earlier capture of the other path (three-launch / one-launch)
+    old = data.get(key, {})
+    for f in ("k_update_bytes_per_launch", "k_forward_bytes_per_launch"):
+        if f not in rec and f in old:
+            rec[f] = old[f]
+            rec.setdefault("earlier_source", {})[f] = old.get("source")
     data[key] = rec
     json.dump(data, open(path, "w"), indent=1, sort_keys=True)
     print(json.dumps(rec, indent=1))
