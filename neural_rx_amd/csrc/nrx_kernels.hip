@@ -2218,6 +2218,12 @@ struct FusedSync {
   // int done[kFusedMaxStages][B] follows
 };
 constexpr int kFusedMaxStages = 4;   // StateInit + up to 3 updates
+#ifndef NRX_DMA_LATE
+#define NRX_DMA_LATE 0
+#endif
+// 1: the next item's z DMA is issued by all eight waves after the item's end barrier instead
+// of by waves 0-3 between the conv3 math and the epilogue
+constexpr bool kDmaLate = NRX_DMA_LATE != 0;
 // dynamic LDS of k_forward: the paired-readout layout minus room for the static __shared__
 // words (the slot-norm reduction of StateInit, the queue words); the readout heads must fit
 constexpr int kFusedLds = 160 * 1024 - 256;
@@ -2310,7 +2316,9 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P16> fp_arg) {
     if (jn < total) decode(jn, sn, bn, un, stn);
     const bool hook = jn < total && sn >= 1;   // the next item's z image can be prefetched
     FusedNext<P> fn{&fp.st[hook ? sn : 0], hook ? done + (sn - 1) * B + bn : nullptr, ips, &sh[2], head, 0};
-    const int nb = hook ? bn : -1, nfs = stn * P::FO - kHalo;
+    const int nfs = stn * P::FO - kHalo;
+    // NRX_DMA_LATE: the body only polls (fn); the DMA goes out after the item (below)
+    const int nb = hook && !kDmaLate ? bn : -1;
     if (s == 0) {
       const auto& a = fp.st[0].a;
       float wm = 1.f;
@@ -2332,6 +2340,9 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P16> fp_arg) {
     have_z = hook && sh[2] != 0;
     fstamp(6);
     if (nrx_tid() == 0) __hip_atomic_fetch_add(done + s * B + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // late DMA: every wave is past the item (barrier above), so the strip image is free; all
+    // eight waves issue the next item's z image, whose prologue waits for it to land
+    if (kDmaLate && have_z) zload_dma_u2<P, 8>(fp.st[sn], X, bn, un, nfs);
     j = jn;
     jn = sh[1];
   }
