@@ -279,8 +279,8 @@ double nrx_flops_per_re_user(const nrx_desc* desc, int32_t num_it);
 /* Per-kernel timing.  While enabled, nrx_forward records a HIP event pair around
  * every kernel launch on the launch stream (not graph-capture safe).  Kernel ids:
  * 0 norm, 1 state-init (+ fused aggregation tail), 2 state-update (+ fused aggregation
- * or readout tail), 3 the one-launch forward (StateInit + updates + readouts; taken for
- * the throughput tier, see nrx_fused_status).
+ * or readout tail), 3 the one-launch forward (StateInit + updates + readouts; see
+ * nrx_fused_status for when it is taken).
  * nrx_profile_enable(h, 1) (re)starts the counters; nrx_profile_read waits for the
  * recorded events and returns the launch count and summed device time of a kernel. */
 int nrx_profile_enable(nrx_handle* h, int32_t enable);

@@ -2227,6 +2227,12 @@ constexpr bool kDmaLate = NRX_DMA_LATE != 0;
 // dynamic LDS of k_forward: the paired-readout layout minus room for the static __shared__
 // words (the slot-norm reduction of StateInit, the queue words); the readout heads must fit
 constexpr int kFusedLds = 160 * 1024 - 256;
+// dynamic LDS of k_forward per strip tier: the 24-row tier's paired-readout layout fills the
+// LDS, so it gives up 256 bytes of WB; the small-grid tiers (8 / 16-row strips) fit whole
+template <class P>
+constexpr int fused_lds() {
+  return strip_lds_bytes<P>(true) > kFusedLds ? kFusedLds : strip_lds_bytes<P>(true);
+}
 constexpr int kFusedMaxB = 65536;
 constexpr size_t kFusedSyncBytes = sizeof(FusedSync) + (size_t)kFusedMaxStages * kFusedMaxB * sizeof(int);
 
@@ -2262,13 +2268,12 @@ __device__ __forceinline__ void fused_wait(const int* cnt, int need, FusedSync* 
   __syncthreads();
 }
 
-template <int A2P, int CHP>
-__global__ __launch_bounds__(512) void k_forward(FusedParams<P16> fp_arg) {
-  using P = P16;
+template <class P, int A2P, int CHP>
+__global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
   // the stage parameters are read through the kernarg segment pointer: indexing the by-value
   // parameter with the (dynamic) stage made the compiler copy the whole struct to scratch
-  typedef const __attribute__((address_space(4))) FusedParams<P16> KFP;
-  const FusedParams<P16>& fp = *(const FusedParams<P16>*)(KFP*)__builtin_amdgcn_kernarg_segment_ptr();
+  typedef const __attribute__((address_space(4))) FusedParams<P> KFP;
+  const FusedParams<P>& fp = *(const FusedParams<P>*)(KFP*)__builtin_amdgcn_kernarg_segment_ptr();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int sh[4];   // 0, 1: dequeued items; 2: next z DMA issued; 3: last workgroup
   constexpr int R0 = strip_slots<P>();
@@ -2712,6 +2717,16 @@ static hipError_t run_rr(const FwdArgs<_Float16, float, _Float16>& args0, const 
   return hipGetLastError();
 }
 
+#ifndef NRX_FUSED_SMALL
+#define NRX_FUSED_SMALL 0
+#endif
+// NRX_FUSED_SMALL=1 (build flag): the small-grid tiers (batch-1 latency) through k_forward as
+// well.  Measured slower (profiles/r03/ab_fused_small_latency.txt): a slot's items all sit on
+// one XCD's queue (the hand-offs stay inside one L2), so a 132-PRB slot runs on 32 CUs
+// instead of 256 (0.093 -> 0.397 ms), and at 4 PRB the dependency waits and un-prefetched
+// z-loads cost more than the two launch boundaries they remove (0.057 -> 0.067 ms).
+constexpr bool kFusedSmall = NRX_FUSED_SMALL != 0;
+
 // NRX_FUSED=0 in the environment (read at every forward) takes the three-launch forward
 // instead of k_forward (A/B and bit-identity tests).
 static bool fused_enabled() {
@@ -2719,20 +2734,25 @@ static bool fused_enabled() {
   return !e || atoi(e) != 0;
 }
 
-// k_forward covers the throughput tier of the bench-type models: 24-row strips with at least
-// two items per CU, U <= 2 (z images are LDS-DMA copies), one StateInit (no Var-IO mix), one
-// LLR head whose readout fits the paired-readout WB layout, 2A <= 16.
+// k_forward covers the bench-type models: U <= 2 (z images are LDS-DMA copies), one StateInit
+// (no Var-IO mix), one LLR head whose readout fits the paired-readout WB layout, 2A <= 16.
+// 24-row strips (throughput tier) need at least two items per CU; the small-grid tiers
+// (8 / 16-row strips, no more items than CUs) take it whatever the count: there it removes
+// the two launch boundaries from a batch-1 forward.
+template <class P>
 static bool fused_applicable(const FwdArgs<_Float16, float, _Float16>& a, int num_it, const void* sync) {
   if (!sync || !fused_enabled()) return false;
-  const long items = (long)a.B * a.U * ((a.F + P16::FO - 1) / P16::FO);
-  return a.U <= 2 && a.num_init == 1 && a.H == 1 && 1 + num_it <= kFusedMaxStages && 2 * a.A <= 16 &&
-         a.B <= kFusedMaxB && items >= 2L * cu_count() && heads_fit_wb(a.bits_max, 16, 2 * a.A) &&
-         30 * kTP * kHID * 2 + kHW2 + 256 * (a.bits_max + 16) <= kFusedLds;
+  const long items = (long)a.B * a.U * ((a.F + P::FO - 1) / P::FO);
+  const bool tier = P::FO != P16::FO || items >= 2L * cu_count();
+  return tier && a.U <= 2 && a.num_init == 1 && a.H == 1 && 1 + num_it <= kFusedMaxStages && 2 * a.A <= 16 &&
+         a.B <= kFusedMaxB && heads_fit_wb(a.bits_max, 16, 2 * a.A) &&
+         strip_slots<P>() * slot_pitch<P>() + kHW2 + 256 * (a.bits_max + 16) <= fused_lds<P>();
 }
 
+template <class P>
 static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, const ModelW<_Float16, float>& W,
                             int num_it, hipStream_t st, Prof* prof, void* sync) {
-  FusedParams<P16> fp{};
+  FusedParams<P> fp{};
   fp.sync = reinterpret_cast<FusedSync*>(sync);
   fp.nst = 1 + num_it;
   const int cus = cu_count();
@@ -2748,12 +2768,12 @@ static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, cons
   }
   FwdArgs<_Float16, float, _Float16> a = args;
   for (int s = 0; s < fp.nst; ++s) {
-    BlockParams<P16>& bp = fp.st[s];
+    BlockParams<P>& bp = fp.st[s];
     bp.inline_combine = 1;
     bp.pair = 0;
     bp.order_rev = 0;
     bp.norm_pre = norm_pre;
-    bp.strips = (args.F + P16::FO - 1) / P16::FO;
+    bp.strips = (args.F + P::FO - 1) / P::FO;
     bp.m = 0;
     for (int h = 0; h < args.H; ++h) {
       bp.llr[h][0] = W.llr[h][0];
@@ -2780,7 +2800,7 @@ static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, cons
     }
     bp.a = a;
   }
-  constexpr int L = kFusedLds;
+  constexpr int L = fused_lds<P>();
 #ifdef NRX_STAMPS
   {
     const int on = getenv("NRX_STAMP_FUSED") ? 100 : 0;
@@ -2789,8 +2809,8 @@ static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, cons
   }
 #endif
   B_(K_FUSED);
-  if (2 * args.A <= 8) k_forward<8, 16><<<cus, 512, L, st>>>(fp);
-  else k_forward<16, 16><<<cus, 512, L, st>>>(fp);
+  if (2 * args.A <= 8) k_forward<P, 8, 16><<<cus, 512, L, st>>>(fp);
+  else k_forward<P, 16, 16><<<cus, 512, L, st>>>(fp);
   E_(K_FUSED);
   return hipGetLastError();
 }
@@ -2799,11 +2819,19 @@ hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args,
                               const ModelW<_Float16, float>& W, const RrImages* rr, int num_it, hipStream_t st,
                               Prof* prof, void* fused_sync) {
   if (NRX_SMALL_STRIPS != 0) {
-    if (small_strips_fit<P16S>(args)) return Launch<P16S>::run(args, W, num_it, st, prof);
-    if (small_strips_fit<P16M>(args)) return Launch<P16M>::run(args, W, num_it, st, prof);
+    if (small_strips_fit<P16S>(args)) {
+      if constexpr (kFusedSmall)
+        if (fused_applicable<P16S>(args, num_it, fused_sync)) return run_fused<P16S>(args, W, num_it, st, prof, fused_sync);
+      return Launch<P16S>::run(args, W, num_it, st, prof);
+    }
+    if (small_strips_fit<P16M>(args)) {
+      if constexpr (kFusedSmall)
+        if (fused_applicable<P16M>(args, num_it, fused_sync)) return run_fused<P16M>(args, W, num_it, st, prof, fused_sync);
+      return Launch<P16M>::run(args, W, num_it, st, prof);
+    }
   }
   if (rr_applicable(args, rr)) return run_rr(args, W, *rr, num_it, st, prof);
-  if (fused_applicable(args, num_it, fused_sync)) return run_fused(args, W, num_it, st, prof, fused_sync);
+  if (fused_applicable<P16>(args, num_it, fused_sync)) return run_fused<P16>(args, W, num_it, st, prof, fused_sync);
   return Launch<P16>::run(args, W, num_it, st, prof);
 }
 
@@ -2839,9 +2867,17 @@ hipError_t setup_kernels() {
     }
   }
   hipError_t e2 = Launch<P64>::setup();
-  for (const void* f : {(const void*)k_forward<8, 16>, (const void*)k_forward<16, 16>}) {
-    hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kFusedLds);
+  auto set_fused = [&](const void* f, int lds) {
+    hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (r != hipSuccess && e2 == hipSuccess) e2 = r;
+  };
+  set_fused((const void*)k_forward<P16, 8, 16>, fused_lds<P16>());
+  set_fused((const void*)k_forward<P16, 16, 16>, fused_lds<P16>());
+  if constexpr (kFusedSmall) {
+    set_fused((const void*)k_forward<P16S, 8, 16>, fused_lds<P16S>());
+    set_fused((const void*)k_forward<P16S, 16, 16>, fused_lds<P16S>());
+    set_fused((const void*)k_forward<P16M, 8, 16>, fused_lds<P16M>());
+    set_fused((const void*)k_forward<P16M, 16, 16>, fused_lds<P16M>());
   }
   return e != hipSuccess ? e : (e1 != hipSuccess ? e1 : e2);
 }

@@ -101,3 +101,4 @@ def test_fused_graph_replay():
         del os.environ["NRX_FUSED"]
     assert np.array_equal(ref["llr_raw"], llr.cpu().numpy())
     assert eng.fused_status(reset=True) == 0
+
