@@ -1805,8 +1805,19 @@ __device__ intx4 g_zero16[1];
 // chunks of one slot); the chunk swizzle is applied on the source address (the lane at
 // physical chunk q' of symbol t loads logical chunk q' ^ swz(t)).  The pe chunk (2 values)
 // is written by ds_write after the DMA has landed.
+// skip (strip kernels): kZSkipPe -- the pe chunk's lanes load nothing (the caller writes that
+// chunk with ds_write once the DMA has landed); kZSkipPads -- neither do the pad symbols
+// t = 14, 15, when the image's pads are zero already (set by an earlier item of the workgroup:
+// the conv layers never write them).  Skipped lanes are EXEC-masked (~18 % fewer lanes per
+// image).  Off (NRX_ZSKIP=0): measured 0.9 % slower than loading the zero chunks
+// (profiles/r03/ab_zdma_skip.txt) -- masked lanes save the DMA no time.
+#ifndef NRX_ZSKIP
+#define NRX_ZSKIP 0
+#endif
+constexpr int kZSkipPe = NRX_ZSKIP ? 1 : 0, kZSkipPads = NRX_ZSKIP ? 2 : 0;
 template <class P, int NW = 8, int W0 = (NRX_DMA_HI ? 8 - NW : 0)>
-__device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X, int b, int u, int f_start) {
+__device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X, int b, int u, int f_start,
+                                             int skip = 0) {
   using S = typename P::S;
   static_assert(sizeof(S) == 2 && kUPD_CINP * 2 / 16 == 16, "f16 z image with 16 chunks per symbol row");
   // the lane's symbol group is fixed at 4 (wave & 3) + tq and instruction k steps by NW: that
@@ -1839,6 +1850,7 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
       lsrc = sp + t * kDS + P::EPC * (q - QS);
     }
   }
+  const bool on = !((skip & kZSkipPe) && t < kT && q == 2 * QS) && !((skip & kZSkipPads) && t >= kT);
   // W0: the first issuing wave (same per-lane sources: the symbol group is wave & 3 either way)
   const int w0 = W0;
   if (wave < w0 || wave >= w0 + NW) return;
@@ -1846,7 +1858,7 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
     const int f = f_start + (k >> 2);             // wave-uniform
     const S* src = reinterpret_cast<const S*>(g_zero16);
     if (f >= 0 && f < F && lsrc) src = lsrc + (size_t)f * (kT * kDS);
-    __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(X + k * 1024), 16, 0, 0);
+    if (on) __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(X + k * 1024), 16, 0, 0);
   }
 }
 
@@ -1855,7 +1867,7 @@ __device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook() {
   if constexpr (kNextHook || kNextHookRO) {
     if (!next_ready()) return;   // fused forward: the next item's inputs were not complete
     if constexpr (NRX_ZSTAGE != 0) zs.commit(X);
-    else zload_dma_u2<P, NRX_DMA_NW>(nprm ? *nprm : *prm, X, nb, nu, nfs);
+    else zload_dma_u2<P, NRX_DMA_NW>(nprm ? *nprm : *prm, X, nb, nu, nfs, kZSkipPe | kZSkipPads);
   }
 }
 
@@ -1865,7 +1877,7 @@ __device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook() {
 template <class P, int CHP, int TAILM>
 __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X, char* WB, int b, int u, int f_start,
                                              int nb, int nu, int nfs, bool issue_z = false,
-                                             FusedNext<P>* fn = nullptr) {
+                                             FusedNext<P>* fn = nullptr, bool pads_zero = false) {
   using S = typename P::S;
   constexpr int R0 = strip_slots<P>();
   constexpr int NQ = kUPD_CINP * (int)sizeof(S) / 16;
@@ -1884,7 +1896,7 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
     pe_v = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + (pe_ok ? pe_f : 0)) * kT + (pe_ok ? pe_t : 0)) * 2);
   // first item of a workgroup: its z DMA goes out behind the conv1-weight and pe loads, so
   // their latency hides under the DMA instead of following it
-  if (issue_z) zload_dma_u2<P>(prm, X, b, u, f_start);
+  if (issue_z) zload_dma_u2<P>(prm, X, b, u, f_start, staged ? 0 : kZSkipPe | (pads_zero ? kZSkipPads : 0));
   stamp(24);
   stamp(25);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2296,6 +2308,7 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
   __syncthreads();
   int j = sh[0], jn = sh[1];
   bool have_z = false;   // item j's z image was DMA'd by the previous item's conv3 hook
+  bool pads_zero = false;   // an earlier item zeroed the strip image's pad symbols
   auto decode = [&](int jj, int& s, int& b, int& u, int& strip) {
     s = jj / per_stage;
     const int k = jj - s * per_stage;
@@ -2333,9 +2346,9 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
       const int fs = strip * P::FO - kHalo;
       if (!have_z) fused_wait(done + (s - 1) * B + b, ips, sy);
       if (s == nst - 1)
-        dma_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn);
+        dma_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn, pads_zero);
       else
-        dma_item_run<P, CHP, TAIL_AGG>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn);
+        dma_item_run<P, CHP, TAIL_AGG>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn, pads_zero);
     }
     fstamp(5);
     // item done: every wave's stores have reached L2, then one add on the slot's counter
@@ -2348,6 +2361,7 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
     // late DMA: every wave is past the item (barrier above), so the strip image is free; all
     // eight waves issue the next item's z image, whose prologue waits for it to land
     if (kDmaLate && have_z) zload_dma_u2<P, 8>(fp.st[sn], X, bn, un, nfs);
+    pads_zero = true;
     j = jn;
     jn = sh[1];
   }
