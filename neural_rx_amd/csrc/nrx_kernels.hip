@@ -2236,6 +2236,10 @@ constexpr int kFusedMaxStages = 4;   // StateInit + up to 3 updates
 // 1: the next item's z DMA is issued by all eight waves after the item's end barrier instead
 // of by waves 0-3 between the conv3 math and the epilogue
 constexpr bool kDmaLate = NRX_DMA_LATE != 0;
+#ifndef NRX_FUSED_PREFETCH
+#define NRX_FUSED_PREFETCH 1
+#endif
+constexpr bool kFusedPrefetch = NRX_FUSED_PREFETCH != 0;
 // dynamic LDS of k_forward: the paired-readout layout minus room for the static __shared__
 // words (the slot-norm reduction of StateInit, the queue words); the readout heads must fit
 constexpr int kFusedLds = 160 * 1024 - 256;
@@ -2332,7 +2336,9 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
 #endif
     int sn = 0, bn = 0, un = 0, stn = 0;
     if (jn < total) decode(jn, sn, bn, un, stn);
-    const bool hook = jn < total && sn >= 1;   // the next item's z image can be prefetched
+    // the next item's z image can be prefetched (NRX_FUSED_PREFETCH=0: never; each update
+    // item then loads its own z image at its start)
+    const bool hook = kFusedPrefetch && jn < total && sn >= 1;
     FusedNext<P> fn{&fp.st[hook ? sn : 0], hook ? done + (sn - 1) * B + bn : nullptr, ips, &sh[2], head, 0};
     const int nfs = stn * P::FO - kHalo;
     // NRX_DMA_LATE: the body only polls (fn); the DMA goes out after the item (below)
