@@ -597,6 +597,9 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
       }
     }
     if (act) epi.template run<R>(acc, pf, p0, t, g, 0, R);
+    if constexpr (E::kNextHook) {
+      if (epi.nb >= 0) epi.next_hook_b();
+    }
     stamp(12 + 5 * in_off);
   } else {
     // rows r >= kEarlyRow of an in-place layer land in slots no other wave reads this
@@ -620,6 +623,9 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
     }
     stamp(11 + 5 * in_off);
     if (act) epi.template run<R>(acc, pf, p0, t, g, 0, ER);
+    if constexpr (E::kNextHookRO) {
+      if (epi.nb >= 0) epi.next_hook_b();
+    }
     stamp(12 + 5 * in_off);
     if (in_off == 0) stamp_w(56);
     __syncthreads();
@@ -1104,6 +1110,7 @@ struct EpiConv3 {
     asm volatile("" : "+v"(act_h));
   }
   __device__ void next_hook();
+  __device__ void next_hook_b();   // NRX_DMA_SPLIT: the second half, after the epilogue
 
   __device__ bool row_ok(int p, int t) const {
     return p >= pos_lo && p < pos_hi && f_start + p < prm->a.F && t < kT;
@@ -1817,7 +1824,7 @@ __device__ intx4 g_zero16[1];
 constexpr int kZSkipPe = NRX_ZSKIP ? 1 : 0, kZSkipPads = NRX_ZSKIP ? 2 : 0;
 template <class P, int NW = 8, int W0 = (NRX_DMA_HI ? 8 - NW : 0)>
 __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X, int b, int u, int f_start,
-                                             int skip = 0) {
+                                             int skip = 0, int wlo = 0, int whi = 8) {
   using S = typename P::S;
   static_assert(sizeof(S) == 2 && kUPD_CINP * 2 / 16 == 16, "f16 z image with 16 chunks per symbol row");
   // the lane's symbol group is fixed at 4 (wave & 3) + tq and instruction k steps by NW: that
@@ -1853,7 +1860,7 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
   const bool on = !((skip & kZSkipPe) && t < kT && q == 2 * QS) && !((skip & kZSkipPads) && t >= kT);
   // W0: the first issuing wave (same per-lane sources: the symbol group is wave & 3 either way)
   const int w0 = W0;
-  if (wave < w0 || wave >= w0 + NW) return;
+  if (wave < w0 || wave >= w0 + NW || wave < wlo || wave >= whi) return;
   for (int k = wave - w0; k < R0 * 4; k += NW) {
     const int f = f_start + (k >> 2);             // wave-uniform
     const S* src = reinterpret_cast<const S*>(g_zero16);
@@ -1862,12 +1869,31 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
   }
 }
 
+// NRX_DMA_SPLIT: the next item's z image goes out in two halves of the eight-wave mapping:
+// waves 0-3 issue theirs before their epilogue (while waves 4-7, their SIMD partners, run
+// theirs), waves 4-7 after their epilogue (while waves 0-3 run theirs), so that every SIMD
+// keeps one wave computing through both halves of the issue stall.  Off: measured 1 % slower
+// than waves 0-3 issuing it all (profiles/r03/ab_fused_dma_placement.txt).
+#ifndef NRX_DMA_SPLIT
+#define NRX_DMA_SPLIT 0
+#endif
+constexpr bool kDmaSplit = NRX_DMA_SPLIT != 0 && NRX_ZSTAGE == 0;
+
 template <class P, class WS, int CHP, int TAILM>
 __device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook() {
   if constexpr (kNextHook || kNextHookRO) {
     if (!next_ready()) return;   // fused forward: the next item's inputs were not complete
     if constexpr (NRX_ZSTAGE != 0) zs.commit(X);
+    else if constexpr (kDmaSplit) zload_dma_u2<P, 8>(nprm ? *nprm : *prm, X, nb, nu, nfs, kZSkipPe | kZSkipPads, 0, 4);
     else zload_dma_u2<P, NRX_DMA_NW>(nprm ? *nprm : *prm, X, nb, nu, nfs, kZSkipPe | kZSkipPads);
+  }
+}
+
+template <class P, class WS, int CHP, int TAILM>
+__device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook_b() {
+  if constexpr ((kNextHook || kNextHookRO) && kDmaSplit) {
+    if (!next_ready()) return;
+    zload_dma_u2<P, 8>(nprm ? *nprm : *prm, X, nb, nu, nfs, kZSkipPe | kZSkipPads, 4, 8);
   }
 }
 
