@@ -1903,7 +1903,8 @@ __device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook_b() {
 template <class P, int CHP, int TAILM>
 __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X, char* WB, int b, int u, int f_start,
                                              int nb, int nu, int nfs, bool issue_z = false,
-                                             FusedNext<P>* fn = nullptr, bool pads_zero = false) {
+                                             FusedNext<P>* fn = nullptr, bool pads_zero = false,
+                                             const SepStage<kUPD_CINP, kHID>* w1pre = nullptr) {
   using S = typename P::S;
   constexpr int R0 = strip_slots<P>();
   constexpr int NQ = kUPD_CINP * (int)sizeof(S) / 16;
@@ -1911,7 +1912,8 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
   const auto& a = prm.a;
   const int F = a.F;
   SepStage<kUPD_CINP, kHID> w1;
-  w1.load(prm.w[0]);
+  if (w1pre) w1 = *w1pre;   // fused forward: loaded at the end of the previous item
+  else w1.load(prm.w[0]);
   // a z image staged by the previous item (ZStage) holds the pe chunk already
   const bool staged = !issue_z && NRX_ZSTAGE != 0;
   const int pe_slot = nrx_tid() / kT, pe_t = nrx_tid() % kT;
@@ -2266,6 +2268,10 @@ constexpr bool kDmaLate = NRX_DMA_LATE != 0;
 #define NRX_FUSED_PREFETCH 1
 #endif
 constexpr bool kFusedPrefetch = NRX_FUSED_PREFETCH != 0;
+#ifndef NRX_W1_PRE
+#define NRX_W1_PRE 0
+#endif
+constexpr bool kW1Pre = NRX_W1_PRE != 0;
 // dynamic LDS of k_forward: the paired-readout layout minus room for the static __shared__
 // words (the slot-norm reduction of StateInit, the queue words); the readout heads must fit
 constexpr int kFusedLds = 160 * 1024 - 256;
@@ -2339,6 +2345,10 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
   int j = sh[0], jn = sh[1];
   bool have_z = false;   // item j's z image was DMA'd by the previous item's conv3 hook
   bool pads_zero = false;   // an earlier item zeroed the strip image's pad symbols
+  // NRX_W1_PRE: the next update item's conv1 weights are loaded at the end of the current
+  // item, so their latency overlaps the item-end store drain instead of the next prologue
+  SepStage<kUPD_CINP, kHID> w1n;
+  bool have_w1 = false;
   auto decode = [&](int jj, int& s, int& b, int& u, int& strip) {
     s = jj / per_stage;
     const int k = jj - s * per_stage;
@@ -2377,12 +2387,15 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
     } else {
       const int fs = strip * P::FO - kHalo;
       if (!have_z) fused_wait(done + (s - 1) * B + b, ips, sy);
+      const SepStage<kUPD_CINP, kHID>* w1p = kW1Pre && have_w1 ? &w1n : nullptr;
       if (s == nst - 1)
-        dma_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn, pads_zero);
+        dma_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn, pads_zero, w1p);
       else
-        dma_item_run<P, CHP, TAIL_AGG>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn, pads_zero);
+        dma_item_run<P, CHP, TAIL_AGG>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn, pads_zero, w1p);
     }
     fstamp(5);
+    have_w1 = kW1Pre && jn < total && sn >= 1;
+    if (have_w1) w1n.load(fp.st[sn].w[0]);
     // item done: every wave's stores have reached L2, then one add on the slot's counter
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (nrx_tid() == 0) sh[1] = fn.jnn;
