@@ -2338,8 +2338,11 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
   const int per_stage = nbq * ips, total = nst * per_stage;
   int* head = &sy->head[q];
   if (nrx_tid() == 0) {
-    sh[0] = atomicAdd(head, 1);
-    sh[1] = atomicAdd(head, 1);
+    // the first two items in one round trip (a second dependent atomic would add its
+    // latency to every workgroup's start)
+    const int j0 = atomicAdd(head, 2);
+    sh[0] = j0;
+    sh[1] = j0 + 1;
   }
   __syncthreads();
   int j = sh[0], jn = sh[1];
