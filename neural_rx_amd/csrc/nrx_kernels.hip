@@ -1443,6 +1443,8 @@ struct FusedNext {
   int* nflag;                   // LDS word: 1 when the next item's z DMA was issued
   int* head;                    // this queue's work counter
   int jnn;                      // thread 0: the item dequeued at the start of this block
+  int* psig = nullptr;          // NRX_SIG_DEFER: the previous item's counter, added once this
+                                // item's prologue has drained every wave's stores
 };
 
 // The three layers of a block, in place: conv1 over positions [1, R0-1), conv2 over
@@ -1929,6 +1931,8 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
   stamp(25);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();   // every wave's DMA has landed (and a previous item's epilogue is done)
+  // fused forward, deferred signal: every wave has drained its stores of the previous item
+  if (fn && fn->psig && nrx_tid() == 0) __hip_atomic_fetch_add(fn->psig, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp(26);
   if (!staged && pe_slot < R0) {
     S pe2[P::EPC] = {};
@@ -2272,6 +2276,12 @@ constexpr bool kFusedPrefetch = NRX_FUSED_PREFETCH != 0;
 #define NRX_W1_PRE 0
 #endif
 constexpr bool kW1Pre = NRX_W1_PRE != 0;
+#ifndef NRX_SIG_DEFER
+#define NRX_SIG_DEFER 0
+#endif
+// 1: an item whose successor's z image was prefetched does not drain its stores at its end;
+// the successor's prologue drains them and adds the counter
+constexpr bool kSigDefer = NRX_SIG_DEFER != 0;
 // dynamic LDS of k_forward: the paired-readout layout minus room for the static __shared__
 // words (the slot-norm reduction of StateInit, the queue words); the readout heads must fit
 constexpr int kFusedLds = 160 * 1024 - 256;
@@ -2352,6 +2362,7 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
   // item, so their latency overlaps the item-end store drain instead of the next prologue
   SepStage<kUPD_CINP, kHID> w1n;
   bool have_w1 = false;
+  int* psig = nullptr;   // NRX_SIG_DEFER: counter of the previous item, not yet added
   auto decode = [&](int jj, int& s, int& b, int& u, int& strip) {
     s = jj / per_stage;
     const int k = jj - s * per_stage;
@@ -2378,7 +2389,7 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
     // the next item's z image can be prefetched (NRX_FUSED_PREFETCH=0: never; each update
     // item then loads its own z image at its start)
     const bool hook = kFusedPrefetch && jn < total && sn >= 1;
-    FusedNext<P> fn{&fp.st[hook ? sn : 0], hook ? done + (sn - 1) * B + bn : nullptr, ips, &sh[2], head, 0};
+    FusedNext<P> fn{&fp.st[hook ? sn : 0], hook ? done + (sn - 1) * B + bn : nullptr, ips, &sh[2], head, 0, psig};
     const int nfs = stn * P::FO - kHalo;
     // NRX_DMA_LATE: the body only polls (fn); the DMA goes out after the item (below)
     const int nb = hook && !kDmaLate ? bn : -1;
@@ -2400,12 +2411,23 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
     have_w1 = kW1Pre && jn < total && sn >= 1;
     if (have_w1) w1n.load(fp.st[sn].w[0]);
     // item done: every wave's stores have reached L2, then one add on the slot's counter
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!kSigDefer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (nrx_tid() == 0) sh[1] = fn.jnn;
     __syncthreads();
     have_z = hook && sh[2] != 0;
     fstamp(6);
-    if (nrx_tid() == 0) __hip_atomic_fetch_add(done + s * B + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    psig = nullptr;
+    if (kSigDefer && have_z) {
+      // the next item runs without a dependency wait: its prologue (vmcnt(0) + barrier on
+      // every wave) releases this item's stores and adds the counter
+      psig = done + s * B + b;
+    } else {
+      if (kSigDefer) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      if (nrx_tid() == 0) __hip_atomic_fetch_add(done + s * B + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // late DMA: every wave is past the item (barrier above), so the strip image is free; all
     // eight waves issue the next item's z image, whose prologue waits for it to land
     if (kDmaLate && have_z) zload_dma_u2<P, 8>(fp.st[sn], X, bn, un, nfs);
