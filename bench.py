@@ -5,6 +5,11 @@
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+Without a launcher, ``--gpus N > 1`` starts the N rank processes itself (a parent that never
+touches the GPU spawns them with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, waits, and
+exits with the worst rank's code), so ``python bench.py --gpus 8`` measures 8 ranks; under a
+launcher WORLD_SIZE must equal --gpus.
+
 Workload (BASELINE.json configs[1]): nrx_rt weights, 2 users, 4 PRB (F = 48), 4 rx
 antennas, 16-QAM, batch 128 slots per GPU, f16 perf mode.  A "step" = one full CGNN
 forward (norm, StateInit, 2 x [aggregation, state update], readouts) over the batch,
@@ -54,17 +59,81 @@ def parse():
                    help="time replays of a captured hipGraph instead of direct nrx_forward calls")
     p.add_argument("--profile-only", action="store_true",
                    help="run warmup + timed steps only (for rocprofv3)")
+    p.add_argument("--selftest", action="store_true",
+                   help="launcher / timing / reduction plumbing only, on the CPU over gloo (no GPU "
+                        "work, no engine): the line it prints is marked and is not a measurement")
     return p.parse_args()
+
+
+def spawn_ranks(n: int) -> int:
+    """--gpus N without a launcher: N child processes, one per GPU, started before this
+    process touches the GPU (it never does); returns the worst exit code.  Only rank 0
+    writes to stdout (the one JSON line)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out = None if r == 0 else subprocess.DEVNULL
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env, stdout=out))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def selftest(args, world, rank):
+    """Plumbing check of the multi-rank path on the CPU (gloo): barrier + timed region + MAX
+    of the elapsed time + whole-job slot count, with a stand-in step (no GPU, no engine)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    x = torch.ones(64, 64)
+    step = lambda: x @ x
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    slots_total = world * args.batch * args.steps
+    if rank == 0:
+        print(json.dumps({"metric": "selftest (launcher plumbing only, not a measurement)", "value":
+                          round(slots_total / elapsed, 1), "unit": "slots/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "slots_total": slots_total, "data": "selftest",
+                          "ranks_spawned_by": os.environ.get("NRX_BENCH_SPAWNED", "launcher")}))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        os.environ["NRX_BENCH_SPAWNED"] = "bench.py"
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: one rank per GPU is required")
+    if args.selftest:
+        selftest(args, world, rank)
+        return
+    import torch
+    import torch.distributed as dist
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local_rank)
@@ -188,6 +257,10 @@ def main():
     peak = metrics.PEAK_TFLOPS[args.precision]
     achieved = dom_flops / dom_avg_s / 1e12
     elem = 2 if args.precision == "f16" else 4
+    # algorithmic bytes = SURVEY 8(d)'s compulsory I/O of one forward (y, h_hat in; LLRs, h_ref
+    # out; f32 as the ABI moves them); the schedule's own state hand-offs between stages are
+    # reported separately (schedule_bytes_per_launch), never as algorithmic
+    compulsory = metrics.compulsory_bytes_per_forward(spec, B, U, F, with_h=True)
     if fused:
         alg_bytes = metrics.forward_bytes_per_re_user(spec, num_it, U, elem) * re_users
         pmc_field, kname = "k_forward_bytes_per_launch", \
@@ -213,12 +286,30 @@ def main():
     pmc_src = None
     if traffic is not None:
         pmc_src = pmc.get(key, {}).get("source")
+    # SQ counters of the dominant kernel from the committed PMC capture (tools/pmc_record.py)
+    sq = {}
+    sq_path = os.path.join(ROOT, "profiles", "pmc_sq.json")
+    if os.path.exists(sq_path):
+        try:
+            sq = json.load(open(sq_path)).get(key, {}).get("k_forward" if fused else "k_update", {})
+        except Exception:
+            sq = {}
     whole_tflops = metrics.forward_flops_per_re_user(spec, num_it) * re_users * world / (elapsed / args.steps) / 1e12
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "kernel": kname,
                 "flops_per_launch": dom_flops,
-                "algorithmic_bytes_per_launch": round(alg_bytes),
+                "algorithmic_bytes_per_launch": compulsory if fused else None,
+                "algorithmic_bytes_kind": "compulsory I/O of the forward (SURVEY 8(d): y, h_hat in, f32 LLRs "
+                                          "and h_ref out, pe once)",
+                "traffic_over_compulsory": round(traffic / compulsory, 3) if (traffic and fused) else None,
+                "schedule_bytes_per_launch": round(alg_bytes),
+                "schedule_bytes_kind": "the schedule's own hand-offs: StateInit reads y, h_hat and writes s, "
+                                       "act*sp; every update reads s, a and writes s', act*sp or the outputs",
+                "mfma_busy_frac": sq.get("mfma_busy_frac"),
+                "valu_issue_frac": sq.get("valu_issue_frac"),
+                "wait_frac": sq.get("wait_frac"),
+                "sq_source": sq.get("source"),
                 "avg_launch_us": round(dom_avg_s * 1e6, 3),
                 "avg_launch_us_event_pairs": kern[dom]["avg_us_event_pairs"],
                 "avg_launch_us_kind": "derived: event-pair share of a step x uninstrumented step time",
@@ -236,8 +327,12 @@ def main():
         upd_items = args.steps * num_it * U * B * ((F + 23) // 24)
         roofline["fused_queue"] = {"update_items_waited": fused_st["waited"], "update_items": upd_items,
                                    "polls": fused_st["polls"], "error": fused_st["error"],
+                                   "ok": fused_st["waited"] == 0 and fused_st["error"] == 0,
                                    "note": "update items whose inputs were not complete when the previous item "
-                                           "polled (z image loaded after a wait, not during that item's epilogue)"}
+                                           "polled (z image loaded after a wait, not during that item's epilogue); "
+                                           "ok = no wait and no error"}
+        if fused_st["error"]:
+            print(f"bench.py: one-launch forward error bits {fused_st['error']}: outputs invalid", file=sys.stderr)
 
     # ---- batch-1 per-slot latency (hipGraph replay; device-only and H2D+compute+D2H)
     latency = None
@@ -467,7 +562,10 @@ def cpu_baseline(spec, cfg, slots, pe_np, args, num_it):
     from neural_rx_amd.config import dmrs_symbols, user_cdm_groups
     from neural_rx_amd.receiver import compute_pe
     model = TorchCGNN(cgnn_ref.split_keras_weights(W.load(cfg.label), spec), spec)
-    all_threads = torch.get_num_threads()
+    # torch.set_num_threads(os.cpu_count()) -- the CPUs this process may run on
+    # (the affinity set; os.cpu_count() where the platform has none)
+    torch_default = torch.get_num_threads()
+    all_threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     B, U = slots.y.shape[0], slots.h_hat.shape[1]
     ones = lambda b, u: np.ones((b, u, spec.num_mcs), np.float32)
     # cfg 1: one user, batch 1 (same trained weights, 4 PRB)
@@ -494,8 +592,9 @@ def cpu_baseline(spec, cfg, slots, pe_np, args, num_it):
         torch.set_num_threads(th)
         res[tag] = {"threads": th, "cfg1_b1_p50_ms": round(p50_b1(40 if th > 1 else 25), 3),
                     "cfg2_b128_slots_per_s": round(b128(2 if th > 1 else 1), 2)}
-    torch.set_num_threads(all_threads)
+    torch.set_num_threads(torch_default)
     return {"value": res["all"]["cfg2_b128_slots_per_s"], "unit": "slots/s", "cores": all_threads,
+            "threads": all_threads, "torch_default_threads": torch_default,
             "kind": "port",
             "sample": f"torch-CPU fp32 restatement (oracle/cgnn_torch.py), bench workload cfg2 "
                       f"({B} slots, {U} users, {args.prbs} PRB, num_it {num_it}) x2 batches at {all_threads} threads "

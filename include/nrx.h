@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NRX_API_VERSION 4
+#define NRX_API_VERSION 5
 
 enum nrx_status {
   NRX_OK = 0,
@@ -47,7 +47,10 @@ enum nrx_status {
   NRX_ERR_UNSUPPORTED = -3,   /* topology the kernels are not built for */
   NRX_ERR_HIP = -4,           /* HIP runtime error (message has the HIP string) */
   NRX_ERR_NOMEM = -5,
-  NRX_ERR_WORKSPACE = -6      /* workspace too small */
+  NRX_ERR_WORKSPACE = -6,     /* workspace too small */
+  NRX_ERR_BUSY = -7,          /* a forward of this handle is still running on another stream */
+  NRX_ERR_FUSED = -8          /* an earlier one-launch forward reported an error: its outputs
+                               * are invalid (see nrx_fused_status) */
 };
 
 /* Arithmetic of a forward pass. */
@@ -292,10 +295,22 @@ int nrx_profile_read(nrx_handle* h, int32_t kernel, int64_t* launches, double* t
  * [0] error bits (1: a bounded dependency wait timed out, 2: items left undone -- the
  * results of that forward are invalid), [1] update items whose inputs were not complete when
  * the previous item polled for them (their z image loaded after a wait instead of during
- * that item's epilogue), [2] the polls those waits took.  Blocking; reset != 0 clears them.
- * Forwards on one handle must not run concurrently on several streams (the counters are
- * per handle).  NRX_FUSED=0 in the environment takes the three-launch path instead. */
+ * that item's epilogue), [2] the polls those waits took.  Blocking: the stream of the last
+ * forward is synchronised first; reset != 0 clears them.  Returns NRX_ERR_FUSED (message
+ * with the bits) when the error word is non-zero, so a caller that only checks the status
+ * code cannot miss it; status[] is filled either way.
+ * Forwards on one handle must not run concurrently on several streams (the counters are per
+ * handle): nrx_forward returns NRX_ERR_BUSY when a forward that would take this path arrives
+ * on a stream other than the previous forward's while that stream still has work pending.
+ * NRX_FUSED=0 in the environment (read by nrx_create) takes the three-launch path instead. */
 int nrx_fused_status(nrx_handle* h, int32_t* status, int32_t reset);
+
+/* Per-handle control of the one-launch forward: enable = 1 / 0 takes it (when applicable) or
+ * the three-launch path (< 0: unchanged; the initial value comes from NRX_FUSED at
+ * nrx_create); spin_limit = dependency-wait polls before the timeout error (<= 0: the
+ * default, ~0.5 s); inject_err = error bits the next forwards set in the error word (test
+ * hook: callers must surface them; 0: none). */
+int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t inject_err);
 
 const char* nrx_last_error(void);
 int32_t nrx_api_version(void);

@@ -14,6 +14,8 @@ LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("NRX_LIB_PATH") or os.path.join(LIB_DIR, "libnrx.so")
 
 NRX_OK = 0
+NRX_ERR_BUSY = -7
+NRX_ERR_FUSED = -8
 NRX_PREC_F16 = 0
 NRX_PREC_F32X = 1
 PRECISIONS = {"f16": NRX_PREC_F16, "fp16": NRX_PREC_F16, "f32x": NRX_PREC_F32X,
@@ -25,7 +27,7 @@ EXPORTS = [
     "nrx_compute_pe", "nrx_flops_per_re_user", "nrx_last_error", "nrx_api_version",
     "nrx_profile_enable", "nrx_profile_read", "nrx_aerial_workspace_size", "nrx_forward_aerial",
     "nrx_llr_demap", "nrx_gen_workspace_size", "nrx_generate_slots", "nrx_count_errors",
-    "nrx_workspace_size_ex", "nrx_forward_ex", "nrx_fused_status",
+    "nrx_workspace_size_ex", "nrx_forward_ex", "nrx_fused_status", "nrx_fused_config",
 ]
 # enum nrx_y_layout
 Y_LAYOUTS = {"cgnn": 0, "sionna": 1, "split": 2}
@@ -219,6 +221,8 @@ def load(path: str = LIB_PATH):
     lib.nrx_profile_read.restype = c.c_int
     lib.nrx_fused_status.argtypes = [c.c_void_p, c.c_void_p, c.c_int32]
     lib.nrx_fused_status.restype = c.c_int
+    lib.nrx_fused_config.argtypes = [c.c_void_p, c.c_int32, c.c_int32, c.c_int32]
+    lib.nrx_fused_config.restype = c.c_int
     lib.nrx_aerial_workspace_size.argtypes = [c.c_void_p, P(nrx_aerial_io), P(c.c_size_t)]
     lib.nrx_aerial_workspace_size.restype = c.c_int
     lib.nrx_forward_aerial.argtypes = [c.c_void_p, P(nrx_aerial_io), c.c_void_p, c.c_size_t, c.c_void_p]

@@ -35,33 +35,52 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in DEPS if os.path.exists(d))
 
 
+HEADERS = [os.path.join(CSRC, "nrx_internal.h"), os.path.join(HERE, "..", "include", "nrx.h")]
+OBJ_DIR = os.path.join(HERE, "lib", "obj")
+
+
+def _stale(obj: str, src: str) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in [src] + HEADERS if os.path.exists(d))
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
+    """Compile the sources whose object is stale (force: all of them), in parallel, then link.
+    Objects are kept in lib/obj/ (git-ignored) so that an edit of one source recompiles only
+    that source."""
     if not force and not needs_build():
         return LIB
-    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    os.makedirs(OBJ_DIR, exist_ok=True)
     tmp = LIB + f".tmp{os.getpid()}"
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
-    # one object per source, compiled in parallel (nrx_kernels.hip dominates), then one link
     objs, procs = [], []
     for src in SOURCES:
-        obj = os.path.join(os.path.dirname(LIB), os.path.basename(src) + f".{os.getpid()}.o")
-        cmd = [hipcc(), *flags, "-c", src, "-o", obj]
-        if verbose:
-            print(" ".join(cmd), flush=True)
+        obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
         objs.append(obj)
-        procs.append(subprocess.Popen(cmd))
-    bad = [p.wait() for p in procs]
-    try:
-        if any(bad):
-            raise subprocess.CalledProcessError(max(bad), "hipcc -c")
-        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", *objs, "-o", tmp]
+        if not force and not _stale(obj, src):
+            continue
+        part = obj + f".{os.getpid()}.part"
+        cmd = [hipcc(), *flags, "-c", src, "-o", part]
         if verbose:
             print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
-    finally:
-        for o in objs:
-            if os.path.exists(o):
-                os.remove(o)
+        procs.append((subprocess.Popen(cmd), part, obj))
+    bad = 0
+    for p, part, obj in procs:
+        rc = p.wait()
+        if rc:
+            bad = rc
+            if os.path.exists(part):
+                os.remove(part)
+        else:
+            os.replace(part, obj)
+    if bad:
+        raise subprocess.CalledProcessError(bad, "hipcc -c")
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", *objs, "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
     return LIB
 

@@ -10,6 +10,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -20,9 +21,10 @@
 
 namespace nrx {
 hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args, const ModelW<_Float16, float>& W,
-                              const RrImages* rr, int num_it, hipStream_t st, Prof* prof, void* fused_sync);
+                              int num_it, hipStream_t st, Prof* prof, const FusedCtl& fc);
+bool fused_would_run(const FwdArgs<_Float16, float, _Float16>& args, int num_it, const FusedCtl& fc);
 size_t fused_sync_bytes();
-hipError_t fused_sync_status(void* sync, int* st, bool reset);
+hipError_t fused_sync_status(void* sync, int* st, bool reset, hipStream_t stream);
 hipError_t launch_forward_f64(const FwdArgs<double, double, float>& args,
                               const ModelW<double, double>& W, int num_it, hipStream_t st,
                               Prof* prof);
@@ -190,57 +192,6 @@ struct DeviceModel {
   ModelW<WT, BT> W{};
   void* dev = nullptr;
   int init_cinp = 0;
-  RrImages rr{};          // f16 model: LDS images for the register-resident kernels
-  void* rr_dev = nullptr;
-};
-
-// LDS images (nrx_internal.h layouts) of the f16 weights, for LDS-DMA by nrx_rr.inc.
-struct ImageBuilder {
-  std::vector<char> blob;
-  size_t add(const std::vector<char>& img) {
-    const size_t off = align256(blob.size());
-    blob.resize(off + img.size());
-    memcpy(blob.data() + off, img.data(), img.size());
-    return off;
-  }
-  // W^T [coutp][cinp] f16 tiles at `base`, rows co < rows
-  static void wt(std::vector<char>& img, int base, const char* w, int cinp, int coutp, int rows) {
-    const int nq = cinp * 2 / 16;
-    for (int co = 0; co < coutp && co < rows; ++co)
-      for (int q = 0; q < nq; ++q)
-        memcpy(img.data() + base + lds_img_off(nq, co >> 4, co & 15, q), w + ((size_t)co * cinp + q * 8) * 2, 16);
-  }
-  // separable layer: pw^T | dw [9][cinp] at kWPw | bias [coutp] f32 at kWBias
-  static std::vector<char> sep(const char* dw, const char* pw, const char* b, int cinp, int coutp) {
-    std::vector<char> img(kRrABytes, 0);
-    wt(img, 0, pw, cinp, coutp, coutp);
-    memcpy(img.data() + kWPw, dw, (size_t)9 * cinp * 2);
-    memcpy(img.data() + kWBias, b, (size_t)coutp * 4);
-    return img;
-  }
-  // aggregation MLP (64 -> 64 -> 64, K permuted): W1^T at 0, W2^T at 8 KB, b1, b2 at kRrTailB
-  static std::vector<char> tail(const char* w1, const char* b1, const char* w2, const char* b2) {
-    std::vector<char> img(kRrTailBytes, 0);
-    wt(img, 0, w1, kDSP, kAGG, kAGG);
-    wt(img, 8 * 1024, w2, kAGG, kDSP, kDSP);
-    memcpy(img.data() + kRrTailB, b1, kAGG * 4);
-    memcpy(img.data() + kRrTailB + kAGG * 4, b2, kDSP * 4);
-    return img;
-  }
-  // readout heads, TAIL_READOUT_WB layout: LLR W1^T | ChEst W1^T | b1 | b2 | W2^T rows
-  static std::vector<char> heads(const char* l1, const char* lb1, const char* l2, const char* lb2, const char* c1,
-                                 const char* cb1, const char* c2, const char* cb2, int bits_max, int a2, int chp) {
-    std::vector<char> img(rr_heads_bytes(bits_max, a2), 0);
-    wt(img, 0, l1, kDSP, kHID, kHID);
-    wt(img, kHW1C, c1, kDSP, kHID, kHID);
-    memcpy(img.data() + kHB1, lb1, kHID * 4);
-    memcpy(img.data() + kHB1 + kHID * 4, cb1, kHID * 4);
-    memcpy(img.data() + kHB2, lb2, 16 * 4);
-    memcpy(img.data() + kHB2 + 16 * 4, cb2, (size_t)chp * 4);
-    wt(img, kHW2, l2, kHID, 16, bits_max);
-    wt(img, kHW2 + bits_max * 256, c2, kHID, chp, a2);
-    return img;
-  }
 };
 
 template <class WT, class BT>
@@ -327,42 +278,6 @@ int build_model(const nrx_desc* d, const float* const* w, int kc, DeviceModel<WT
   }
   out->W.chest[0] = fd(ch[0]);
   out->W.chest[1] = fd(ch[1]);
-  if constexpr (std::is_same<WT, _Float16>::value) {
-    // LDS images for the register-resident kernels, built from the packed blob
-    const char* hb = pk.blob.data();
-    ImageBuilder ib;
-    size_t o_init[kMaxInit][3] = {}, o_upd[kMaxIt][3] = {}, o_tail[kMaxIt] = {}, o_heads = 0;
-    for (int m = 0; m < num_init(d); ++m)
-      for (int l = 0; l < 3; ++l) {
-        const int cinp = l == 0 ? icinp : kHID, coutp = l == 2 ? kDSP : kHID;
-        o_init[m][l] = ib.add(ImageBuilder::sep(hb + init[m][l].dw, hb + init[m][l].pw, hb + init[m][l].b, cinp, coutp));
-      }
-    for (int i = 0; i < d->num_it; ++i) {
-      for (int l = 0; l < 3; ++l) {
-        const int cinp = l == 0 ? kUPD_CINP : kHID, coutp = l == 2 ? kDSP : kHID;
-        o_upd[i][l] = ib.add(ImageBuilder::sep(hb + upd[i][l].dw, hb + upd[i][l].pw, hb + upd[i][l].b, cinp, coutp));
-      }
-      o_tail[i] = ib.add(ImageBuilder::tail(hb + agg[i][0].w, hb + agg[i][0].b, hb + agg[i][1].w, hb + agg[i][1].b));
-    }
-    const int bm = bits_max(d), chp = a2 <= 16 ? 16 : 32;
-    const bool heads = num_heads(d) == 1 && rr_heads_bytes(bm, a2) <= kRrBBytes && chp == 16;
-    if (heads)
-      o_heads = ib.add(ImageBuilder::heads(hb + llr[0][0].w, hb + llr[0][0].b, hb + llr[0][1].w, hb + llr[0][1].b,
-                                           hb + ch[0].w, hb + ch[0].b, hb + ch[1].w, hb + ch[1].b, bm, a2, chp));
-    e = hipMalloc(&out->rr_dev, ib.blob.size());
-    if (e != hipSuccess) return hip_fail(e, "hipMalloc(rr images)");
-    e = hipMemcpy(out->rr_dev, ib.blob.data(), ib.blob.size(), hipMemcpyHostToDevice);
-    if (e != hipSuccess) return hip_fail(e, "hipMemcpy(rr images)");
-    const char* rb = (const char*)out->rr_dev;
-    for (int m = 0; m < num_init(d); ++m)
-      for (int l = 0; l < 3; ++l) out->rr.init[m][l] = rb + o_init[m][l];
-    for (int i = 0; i < d->num_it; ++i) {
-      for (int l = 0; l < 3; ++l) out->rr.upd[i][l] = rb + o_upd[i][l];
-      out->rr.tail[i] = rb + o_tail[i];
-    }
-    out->rr.heads = heads ? rb + o_heads : nullptr;
-    out->rr.heads_bytes = heads ? rr_heads_bytes(bm, a2) : 0;
-  }
   return NRX_OK;
 }
 
@@ -433,6 +348,12 @@ struct nrx_handle {
   DeviceModel<double, double> m64;
   EventProf* prof = nullptr;
   void* fused_sync = nullptr;   // k_forward's work queues and dependency counters (zeroed)
+  bool fused_enabled = true;    // NRX_FUSED (environment, read once at nrx_create)
+  int spin_limit = kFusedSpinLimit;
+  int dbg_err = 0;
+  hipStream_t last_stream = nullptr;   // stream of the last one-launch forward
+  bool have_last = false;
+  FusedCtl fused_ctl() const { return FusedCtl{fused_sync, fused_enabled, spin_limit, dbg_err}; }
 };
 
 static size_t state_bytes(const nrx_shape* s, int precision) {
@@ -523,6 +444,10 @@ int nrx_create(const nrx_desc* desc, const float* const* weights, const int64_t*
   nrx_handle* h = new nrx_handle();
   h->desc = *desc;
   h->device = device;
+  {
+    const char* ev = getenv("NRX_FUSED");   // A/B and bit-identity tests: 0 = three launches
+    h->fused_enabled = !ev || atoi(ev) != 0;
+  }
   e = hipMalloc(&h->fused_sync, fused_sync_bytes());
   if (e == hipSuccess) e = hipMemset(h->fused_sync, 0, fused_sync_bytes());
   if (e != hipSuccess) {
@@ -542,7 +467,6 @@ int nrx_create(const nrx_desc* desc, const float* const* weights, const int64_t*
 void nrx_destroy(nrx_handle* h) {
   if (!h) return;
   if (h->m16.dev) (void)hipFree(h->m16.dev);
-  if (h->m16.rr_dev) (void)hipFree(h->m16.rr_dev);
   if (h->m64.dev) (void)hipFree(h->m64.dev);
   if (h->fused_sync) (void)hipFree(h->fused_sync);
   delete h->prof;
@@ -577,7 +501,19 @@ int nrx_forward(nrx_handle* h, const nrx_io* io, void* workspace, size_t workspa
   if (io->precision == NRX_PREC_F16) {
     FwdArgs<_Float16, float, _Float16> a{};
     fill_args(a, h, io, workspace, h->m16.init_cinp);
-    e = launch_forward_f16(a, h->m16.W, &h->m16.rr, io->num_it, st, h->prof, h->fused_sync);
+    const FusedCtl fc = h->fused_ctl();
+    if (fused_would_run(a, io->num_it, fc)) {
+      // one stream per handle on this path (the counters are per handle): a forward on another
+      // stream is refused while the previous one's stream still has work
+      if (h->have_last && h->last_stream != st) {
+        const hipError_t q = hipStreamQuery(h->last_stream);
+        if (q == hipErrorNotReady)
+          return fail(NRX_ERR_BUSY, "a one-launch forward of this handle is still running on another stream");
+      }
+      h->last_stream = st;
+      h->have_last = true;
+    }
+    e = launch_forward_f16(a, h->m16.W, io->num_it, st, h->prof, fc);
   } else {
     FwdArgs<double, double, float> a{};
     fill_args(a, h, io, workspace, h->m64.init_cinp);
@@ -830,9 +766,20 @@ int nrx_profile_enable(nrx_handle* h, int32_t enable) {
 int nrx_fused_status(nrx_handle* h, int32_t* status, int32_t reset) {
   if (!h || !status) return fail(NRX_ERR_INVALID_ARG, "null argument");
   int st[3] = {0, 0, 0};
-  hipError_t e = fused_sync_status(h->fused_sync, st, reset != 0);
+  hipError_t e = fused_sync_status(h->fused_sync, st, reset != 0, h->have_last ? h->last_stream : nullptr);
   if (e != hipSuccess) return hip_fail(e, "fused status");
   for (int i = 0; i < 3; ++i) status[i] = st[i];
+  if (st[0])
+    return fail(NRX_ERR_FUSED, "one-launch forward error bits " + std::to_string(st[0]) +
+                                   " (1: dependency wait timed out, 2: items left undone): outputs invalid");
+  return NRX_OK;
+}
+
+int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t inject_err) {
+  if (!h) return fail(NRX_ERR_INVALID_ARG, "null argument");
+  if (enable >= 0) h->fused_enabled = enable != 0;
+  h->spin_limit = spin_limit > 0 ? spin_limit : kFusedSpinLimit;
+  h->dbg_err = inject_err;
   return NRX_OK;
 }
 

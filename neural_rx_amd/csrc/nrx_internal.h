@@ -30,8 +30,7 @@ constexpr int kMaxHeads = 8;
 constexpr int kMaxUsers = 16;
 constexpr int kHalo = 3;      // 3 stacked 3x3 convs per block
 
-// ---- LDS images of the f16 weights (kernels: SepStage / DenseStage / nrx_rr.inc DMA;
-// host: nrx_api.cpp packs the same bytes for LDS-DMA).  A W^T [COUTP][CINP] image is a stack
+// ---- LDS images of the f16 weights (kernels: SepStage / DenseStage).  A W^T [COUTP][CINP] image is a stack
 // of 16-row tiles addressed like an activation image: element (co, chunk q of 8 inputs) at
 // lds_off<NQ>(co >> 4, co & 15, q), NQ = CINP / 8 chunks per row, chunk index XOR-swizzled
 // with the row so that a ds_read_b128 lane group hits distinct bank slots.
@@ -54,22 +53,6 @@ constexpr int kHW1C = 16 * 1024;                 // ChEst W1^T (LLR W1^T at 0)
 constexpr int kHB1 = 32 * 1024;                  // b1: LLR [128] f32, ChEst [128] f32
 constexpr int kHB2 = kHB1 + 2 * kHID * 4;        // b2: LLR [16] f32, ChEst [<= 32] f32
 constexpr int kHW2 = kHB2 + (16 + 32) * 4;       // LLR W2^T rows [bits], then ChEst rows [2A]
-// register-resident blocks (nrx_rr.inc): a sep image without the tail biases, the
-// aggregation-MLP tail image (W1^T 64x64 | W2^T 64x64 | b1 | b2), the heads image budget
-constexpr int kRrABytes = kWPw + kWDw + kHID * 4;   // 35 584
-constexpr int kRrBBytes = 37632;
-constexpr int kRrTailB = kWTailBias - 16 * 1024;    // 18 944
-constexpr int kRrTailBytes = kRrTailB + 2 * kAGG * 4;
-__host__ __device__ constexpr int rr_heads_bytes(int bits_max, int a2) { return kHW2 + 256 * (bits_max + a2); }
-
-// Device copies of the LDS images (f16 model; null where a layer has none).
-struct RrImages {
-  const char* init[kMaxInit][3];
-  const char* upd[kMaxIt][3];
-  const char* tail[kMaxIt];     // aggregation MLP of iteration i
-  const char* heads;            // LLR head 0 + ChEst (one LLR head only), or null
-  int heads_bytes;
-};
 
 template <class WT, class BT>
 struct SepW {
@@ -116,6 +99,17 @@ struct FwdArgs {
   S* a;                            // aggregate read by this update
   S* a_out;                        // aggregate written by the tail
 };
+
+// The one-launch forward's control block (nrx_api.cpp fills it from the handle): the
+// work-queue / counter buffer, whether the path may run (NRX_FUSED, read once at nrx_create),
+// the dependency-wait bound and debug error bits (nrx_debug_fused).
+struct FusedCtl {
+  void* sync;
+  bool enabled;
+  int spin_limit;
+  int dbg_err;
+};
+constexpr int kFusedSpinLimit = 1 << 21;   // ~0.5 s of s_sleep 4 polls
 
 // Optional per-kernel timing (nrx_profile_enable): events recorded around each launch on
 // the launch stream.  Kernel ids:

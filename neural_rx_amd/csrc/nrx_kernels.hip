@@ -563,7 +563,6 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
   typename E::template PrefT<R> pf;
   stamp(8 + 5 * in_off);
   if (act) epi.template prefetch<R>(pf, p0, t, g);   // epilogue global loads, in flight during the math
-  if constexpr (E::kNextHook || E::kNextHookRO) epi.stage_next();
   if (act) {
     if constexpr (NRX_ABLATE & 1) {
 #pragma unroll
@@ -597,9 +596,6 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
       }
     }
     if (act) epi.template run<R>(acc, pf, p0, t, g, 0, R);
-    if constexpr (E::kNextHook) {
-      if (epi.nb >= 0) epi.next_hook_b();
-    }
     stamp(12 + 5 * in_off);
   } else {
     // rows r >= kEarlyRow of an in-place layer land in slots no other wave reads this
@@ -623,9 +619,6 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
     }
     stamp(11 + 5 * in_off);
     if (act) epi.template run<R>(acc, pf, p0, t, g, 0, ER);
-    if constexpr (E::kNextHookRO) {
-      if (epi.nb >= 0) epi.next_hook_b();
-    }
     stamp(12 + 5 * in_off);
     if (in_off == 0) stamp_w(56);
     __syncthreads();
@@ -968,85 +961,6 @@ __device__ __forceinline__ int head_w2(int h) { return head_w1(h) + 16 * 1024; }
 __device__ __forceinline__ int head_b1(int h) { return head_w1(h) + kHeadSlot; }
 __device__ __forceinline__ int head_b2(int h) { return head_b1(h) + 512; }
 
-#ifndef NRX_ZSTAGE
-#define NRX_ZSTAGE 0   // 1: register-staged next-item z image (measured slower)
-#endif
-
-// The z image [a | s | pe] of a workgroup's NEXT update item (U <= 2: a = the other user's
-// act*sp plane, or 0), staged through registers.  The loads are issued at the start of the
-// current item's conv3 layer -- 64 output channels, so ~60 VGPRs are free there -- and their
-// latency hides behind the conv3 math; once every wave is past its conv3 reads the values are
-// written into the strip image (commit), before the epilogue.  The LDS-DMA it replaces issued
-// 123 KB after the conv3 math and held the issuing waves ~6.5 k cycles (profiles/r02/
-// stamps_pair_dma.txt).  Per 16-row slot of a (b, u) plane the in-grid rows are contiguous
-// (14 symbols x 7 chunks), so thread c of the concatenated a | s chunk range loads chunk c:
-// coalesced 16-byte loads, 12 per thread.  Out-of-grid rows and the missing plane are zeros;
-// the pad symbols t = 14, 15 of the strip image are zero already (set at the workgroup's first
-// item, never written by the conv layers) and are not touched.
-template <class P>
-struct ZStage {
-  using S = typename P::S;
-  static constexpr int R0 = strip_slots<P>();
-  static constexpr int QS = kDS / 8;                 // chunks of a plane row per symbol (7)
-  static constexpr int ROWC = kT * QS;               // chunks per grid row (98)
-  static constexpr int PLANE = R0 * ROWC;            // chunks of one plane over the strip
-  static constexpr int NL = (2 * PLANE + 511) / 512;
-  static constexpr int NPE = R0 * kT;                // (slot, t < 14) pairs: pe + zero chunks
-  static_assert(NPE <= 512, "one pe chunk per thread");
-  intx4 v[NL];
-  float2 pe;
-  int f_start, F, U;
-  // raw loads only: every mask is applied in commit -- a select here made the compiler wait
-  // for the loads right at the start of the conv3 math
-  __device__ void issue(const BlockParams<P>& np, int b, int u, int fs) {
-    const auto& a = np.a;
-    f_start = fs;
-    F = a.F;
-    U = a.U;
-    const int tid = nrx_tid();
-    const S* sp = a.s_in + srow(b, u, 0, 0, U, F);
-    const S* ap = U == 2 ? a.a + srow(b, 1 - u, 0, 0, U, F) : sp;
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const int c = tid + 512 * i;
-      const int pl = c >= PLANE;
-      const int k = c - pl * PLANE;
-      const int f = f_start + k / ROWC;
-      const bool ok = c < 2 * PLANE && f >= 0 && f < F;
-      // unconditional load from a clamped address (no branch around it)
-      const unsigned off = ok ? (unsigned)(f * ROWC + k % ROWC) : 0u;
-      v[i] = reinterpret_cast<const intx4*>(pl ? sp : ap)[off];
-    }
-    const int slot = tid / kT, t = tid % kT, f = f_start + slot;
-    const bool ok = tid < NPE && f >= 0 && f < F;
-    pe = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + (ok ? f : 0)) * kT + (ok ? t : 0)) * 2);
-  }
-  __device__ void commit(char* X) const {
-    const int tid = nrx_tid();
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const int c = tid + 512 * i;
-      if (c < 2 * PLANE) {
-        const int pl = c >= PLANE;
-        const int k = c - pl * PLANE;
-        const int slot = k / ROWC, t = (k % ROWC) / QS, q = k % QS + pl * QS;
-        const int f = f_start + slot;
-        const bool ok = f >= 0 && f < F && (pl || U == 2);
-        *reinterpret_cast<intx4*>(X + xoff<P, 16>(slot, t, q)) = ok ? v[i] : intx4{0, 0, 0, 0};
-      }
-    }
-    if (tid < NPE) {
-      const int slot = tid / kT, t = tid % kT, f = f_start + slot;
-      const bool ok = f >= 0 && f < F;
-      S pe2[P::EPC] = {};
-      pe2[0] = ok ? (S)pe.x : (S)0;
-      pe2[1] = ok ? (S)pe.y : (S)0;
-      *reinterpret_cast<intx4*>(X + xoff<P, 16>(slot, t, 2 * QS)) = *reinterpret_cast<const intx4*>(pe2);
-      *reinterpret_cast<intx4*>(X + xoff<P, 16>(slot, t, 2 * QS + 1)) = intx4{0, 0, 0, 0};
-    }
-  }
-};
-
 #ifndef NRX_RO_STRAIGHT
 #define NRX_RO_STRAIGHT 1
 #endif
@@ -1089,15 +1003,8 @@ struct EpiConv3 {
   const BlockParams<P>* nprm = nullptr;
   const int* ndone = nullptr;
   int* nflag = nullptr;
-  ZStage<P> zs;   // the next item's z image in flight (NRX_ZSTAGE)
 
   __device__ bool next_ready() const { return nb >= 0 && (!ndone || *nflag); }
-  // conv3 start, every thread: the next item's z loads (their latency hides behind the math)
-  __device__ void stage_next() {
-    if constexpr (NRX_ZSTAGE != 0 && (kNextHook || kNextHookRO)) {
-      if (next_ready()) zs.issue(nprm ? *nprm : *prm, nb, nu, nfs);
-    }
-  }
 
   template <int R>
   __device__ void settle(PrefT<R>& pf) {
@@ -1110,7 +1017,6 @@ struct EpiConv3 {
     asm volatile("" : "+v"(act_h));
   }
   __device__ void next_hook();
-  __device__ void next_hook_b();   // NRX_DMA_SPLIT: the second half, after the epilogue
 
   __device__ bool row_ok(int p, int t) const {
     return p >= pos_lo && p < pos_hi && f_start + p < prm->a.F && t < kT;
@@ -1443,8 +1349,6 @@ struct FusedNext {
   int* nflag;                   // LDS word: 1 when the next item's z DMA was issued
   int* head;                    // this queue's work counter
   int jnn;                      // thread 0: the item dequeued at the start of this block
-  int* psig = nullptr;          // NRX_SIG_DEFER: the previous item's counter, added once this
-                                // item's prologue has drained every wave's stores
 };
 
 // The three layers of a block, in place: conv1 over positions [1, R0-1), conv2 over
@@ -1490,7 +1394,7 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
     // fused forward: thread 0 polls the next item's dependency counter (an sc1 load, L2-
     // served) and invalidates this CU's L1 -- no line of the next item's inputs this CU read
     // in an earlier stage (ping-pong buffers) may survive into its loads; both complete
-    // behind the conv2 math.  The verdict goes to nflag for conv3's stage_next / next_hook.
+    // behind the conv2 math.  The verdict goes to nflag for conv3's next_hook.
     int pv = 0;
     const bool poll = fn && fn->ndone && nrx_tid() == 0;
     if (poll) {
@@ -1788,15 +1692,11 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
   stamp(4);
 }
 
-// Waves that issue the paired next item's z DMA (0 .. NW-1; 8: all).  A burst of LDS-DMA
-// issues stalls the issuing wave; with NW = 4 one wave of each SIMD pair issues while the
-// other runs its epilogue.
-#ifndef NRX_DMA_NW
-#define NRX_DMA_NW 4
-#endif
-#ifndef NRX_DMA_HI
-#define NRX_DMA_HI 0
-#endif
+// Waves that issue the paired next item's z DMA: 0-3.  A burst of LDS-DMA issues stalls the
+// issuing wave; with four issuing waves one wave of each SIMD pair issues while the other runs
+// its epilogue (all eight: -1.5 %, after the item: -2.1 %, split before / after the epilogue:
+// -1 %; profiles/r03/ab_fused_dma_placement.txt).
+constexpr int kDmaWaves = 4;
 
 // 16 zero bytes: the LDS-DMA source of every z chunk that is zero (pad symbols, rows
 // outside the grid, channel padding, the missing other user of U = 1)
@@ -1813,27 +1713,17 @@ __device__ intx4 g_zero16[1];
 // store instructions.  One wave-instruction fills 1 KB of LDS linearly (4 symbols x 16
 // chunks of one slot); the chunk swizzle is applied on the source address (the lane at
 // physical chunk q' of symbol t loads logical chunk q' ^ swz(t)).  The pe chunk (2 values)
-// is written by ds_write after the DMA has landed.
-// skip (strip kernels): kZSkipPe -- the pe chunk's lanes load nothing (the caller writes that
-// chunk with ds_write once the DMA has landed); kZSkipPads -- neither do the pad symbols
-// t = 14, 15, when the image's pads are zero already (set by an earlier item of the workgroup:
-// the conv layers never write them).  Skipped lanes are EXEC-masked (~18 % fewer lanes per
-// image).  Off (NRX_ZSKIP=0): measured 0.9 % slower than loading the zero chunks
-// (profiles/r03/ab_zdma_skip.txt) -- masked lanes save the DMA no time.
-#ifndef NRX_ZSKIP
-#define NRX_ZSKIP 0
-#endif
-constexpr int kZSkipPe = NRX_ZSKIP ? 1 : 0, kZSkipPads = NRX_ZSKIP ? 2 : 0;
-template <class P, int NW = 8, int W0 = (NRX_DMA_HI ? 8 - NW : 0)>
-__device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X, int b, int u, int f_start,
-                                             int skip = 0, int wlo = 0, int whi = 8) {
+// is written by ds_write after the DMA has landed.  Every lane loads (zero chunks from
+// g_zero16): EXEC-masking the pe / pad-symbol lanes was 0.9 % slower (profiles/r03/
+// ab_zdma_skip.txt).
+template <class P, int NW = 8>
+__device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X, int b, int u, int f_start) {
   using S = typename P::S;
   static_assert(sizeof(S) == 2 && kUPD_CINP * 2 / 16 == 16, "f16 z image with 16 chunks per symbol row");
   // the lane's symbol group is fixed at 4 (wave & 3) + tq and instruction k steps by NW: that
   // matches k's symbol group 4 (k & 3) + tq only when NW is a multiple of 4 and the issuing
-  // waves w0 .. w0+NW-1 are 8-aligned as a set of residues mod 4
+  // waves 0 .. NW-1 cover every residue mod 4
   static_assert(NW % 4 == 0 && NW <= 8, "DMA-issuing wave count must be 4 or 8");
-  static_assert(W0 % 4 == 0 && W0 + NW <= 8, "issuing waves: 0-3, 4-7 or all 8");
   constexpr int R0 = strip_slots<P>();
   constexpr int QS = kDS / P::EPC;   // 7 chunks of a, then 7 of s
   const auto& a = prm.a;
@@ -1859,43 +1749,20 @@ __device__ __forceinline__ void zload_dma_u2(const BlockParams<P>& prm, char* X,
       lsrc = sp + t * kDS + P::EPC * (q - QS);
     }
   }
-  const bool on = !((skip & kZSkipPe) && t < kT && q == 2 * QS) && !((skip & kZSkipPads) && t >= kT);
-  // W0: the first issuing wave (same per-lane sources: the symbol group is wave & 3 either way)
-  const int w0 = W0;
-  if (wave < w0 || wave >= w0 + NW || wave < wlo || wave >= whi) return;
-  for (int k = wave - w0; k < R0 * 4; k += NW) {
+  if (wave >= NW) return;
+  for (int k = wave; k < R0 * 4; k += NW) {
     const int f = f_start + (k >> 2);             // wave-uniform
     const S* src = reinterpret_cast<const S*>(g_zero16);
     if (f >= 0 && f < F && lsrc) src = lsrc + (size_t)f * (kT * kDS);
-    if (on) __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(X + k * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(X + k * 1024), 16, 0, 0);
   }
 }
-
-// NRX_DMA_SPLIT: the next item's z image goes out in two halves of the eight-wave mapping:
-// waves 0-3 issue theirs before their epilogue (while waves 4-7, their SIMD partners, run
-// theirs), waves 4-7 after their epilogue (while waves 0-3 run theirs), so that every SIMD
-// keeps one wave computing through both halves of the issue stall.  Off: measured 1 % slower
-// than waves 0-3 issuing it all (profiles/r03/ab_fused_dma_placement.txt).
-#ifndef NRX_DMA_SPLIT
-#define NRX_DMA_SPLIT 0
-#endif
-constexpr bool kDmaSplit = NRX_DMA_SPLIT != 0 && NRX_ZSTAGE == 0;
 
 template <class P, class WS, int CHP, int TAILM>
 __device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook() {
   if constexpr (kNextHook || kNextHookRO) {
     if (!next_ready()) return;   // fused forward: the next item's inputs were not complete
-    if constexpr (NRX_ZSTAGE != 0) zs.commit(X);
-    else if constexpr (kDmaSplit) zload_dma_u2<P, 8>(nprm ? *nprm : *prm, X, nb, nu, nfs, kZSkipPe | kZSkipPads, 0, 4);
-    else zload_dma_u2<P, NRX_DMA_NW>(nprm ? *nprm : *prm, X, nb, nu, nfs, kZSkipPe | kZSkipPads);
-  }
-}
-
-template <class P, class WS, int CHP, int TAILM>
-__device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook_b() {
-  if constexpr ((kNextHook || kNextHookRO) && kDmaSplit) {
-    if (!next_ready()) return;
-    zload_dma_u2<P, 8>(nprm ? *nprm : *prm, X, nb, nu, nfs, kZSkipPe | kZSkipPads, 4, 8);
+    zload_dma_u2<P, kDmaWaves>(nprm ? *nprm : *prm, X, nb, nu, nfs);
   }
 }
 
@@ -1905,8 +1772,7 @@ __device__ void EpiConv3<P, WS, CHP, TAILM>::next_hook_b() {
 template <class P, int CHP, int TAILM>
 __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X, char* WB, int b, int u, int f_start,
                                              int nb, int nu, int nfs, bool issue_z = false,
-                                             FusedNext<P>* fn = nullptr, bool pads_zero = false,
-                                             const SepStage<kUPD_CINP, kHID>* w1pre = nullptr) {
+                                             FusedNext<P>* fn = nullptr) {
   using S = typename P::S;
   constexpr int R0 = strip_slots<P>();
   constexpr int NQ = kUPD_CINP * (int)sizeof(S) / 16;
@@ -1914,27 +1780,20 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
   const auto& a = prm.a;
   const int F = a.F;
   SepStage<kUPD_CINP, kHID> w1;
-  if (w1pre) w1 = *w1pre;   // fused forward: loaded at the end of the previous item
-  else w1.load(prm.w[0]);
-  // a z image staged by the previous item (ZStage) holds the pe chunk already
-  const bool staged = !issue_z && NRX_ZSTAGE != 0;
+  w1.load(prm.w[0]);
   const int pe_slot = nrx_tid() / kT, pe_t = nrx_tid() % kT;
   const int pe_f = f_start + pe_slot;
   const bool pe_ok = pe_slot < R0 && pe_f >= 0 && pe_f < F;
-  float2 pe_v = float2{0.f, 0.f};
-  if (!staged)
-    pe_v = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + (pe_ok ? pe_f : 0)) * kT + (pe_ok ? pe_t : 0)) * 2);
+  const float2 pe_v = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + (pe_ok ? pe_f : 0)) * kT + (pe_ok ? pe_t : 0)) * 2);
   // first item of a workgroup: its z DMA goes out behind the conv1-weight and pe loads, so
   // their latency hides under the DMA instead of following it
-  if (issue_z) zload_dma_u2<P>(prm, X, b, u, f_start, staged ? 0 : kZSkipPe | (pads_zero ? kZSkipPads : 0));
+  if (issue_z) zload_dma_u2<P>(prm, X, b, u, f_start);
   stamp(24);
   stamp(25);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();   // every wave's DMA has landed (and a previous item's epilogue is done)
-  // fused forward, deferred signal: every wave has drained its stores of the previous item
-  if (fn && fn->psig && nrx_tid() == 0) __hip_atomic_fetch_add(fn->psig, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp(26);
-  if (!staged && pe_slot < R0) {
+  if (pe_slot < R0) {
     S pe2[P::EPC] = {};
     pe2[0] = pe_ok ? (S)pe_v.x : (S)0;
     pe2[1] = pe_ok ? (S)pe_v.y : (S)0;
@@ -2262,26 +2121,6 @@ struct FusedSync {
   // int done[kFusedMaxStages][B] follows
 };
 constexpr int kFusedMaxStages = 4;   // StateInit + up to 3 updates
-#ifndef NRX_DMA_LATE
-#define NRX_DMA_LATE 0
-#endif
-// 1: the next item's z DMA is issued by all eight waves after the item's end barrier instead
-// of by waves 0-3 between the conv3 math and the epilogue
-constexpr bool kDmaLate = NRX_DMA_LATE != 0;
-#ifndef NRX_FUSED_PREFETCH
-#define NRX_FUSED_PREFETCH 1
-#endif
-constexpr bool kFusedPrefetch = NRX_FUSED_PREFETCH != 0;
-#ifndef NRX_W1_PRE
-#define NRX_W1_PRE 0
-#endif
-constexpr bool kW1Pre = NRX_W1_PRE != 0;
-#ifndef NRX_SIG_DEFER
-#define NRX_SIG_DEFER 0
-#endif
-// 1: an item whose successor's z image was prefetched does not drain its stores at its end;
-// the successor's prologue drains them and adds the counter
-constexpr bool kSigDefer = NRX_SIG_DEFER != 0;
 // dynamic LDS of k_forward: the paired-readout layout minus room for the static __shared__
 // words (the slot-norm reduction of StateInit, the queue words); the readout heads must fit
 constexpr int kFusedLds = 160 * 1024 - 256;
@@ -2300,6 +2139,8 @@ struct FusedParams {
   FusedSync* sync;
   int nst;                              // 1 + num_it
   int nq;                               // queues (XCDs)
+  int spin_limit;                       // dependency-wait polls before the timeout error
+  int dbg_err;                          // debug: error bits workgroup 0 sets (nrx_debug_fused)
 };
 
 __device__ __forceinline__ int xcc_id() {
@@ -2308,12 +2149,12 @@ __device__ __forceinline__ int xcc_id() {
 
 // Thread 0 waits for *cnt >= need (bounded), then invalidates this CU's L1 before the
 // workgroup loads the handed-off rows.
-__device__ __forceinline__ void fused_wait(const int* cnt, int need, FusedSync* sy) {
+__device__ __forceinline__ void fused_wait(const int* cnt, int need, FusedSync* sy, int limit) {
   if (nrx_tid() == 0) {
     int it = 0;
     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
       __builtin_amdgcn_s_sleep(4);
-      if (++it > (1 << 21)) {
+      if (++it > limit) {
         __hip_atomic_fetch_or(&sy->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -2339,7 +2180,7 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
   char* WB = smem + R0 * slot_pitch<P>();
   FusedSync* sy = fp_arg.sync;   // scalars straight from the parameter (keeps it in the kernarg list)
   int* done = reinterpret_cast<int*>(sy + 1);
-  const int nst = fp_arg.nst, nqs = fp_arg.nq;
+  const int nst = fp_arg.nst, nqs = fp_arg.nq, spin_limit = fp_arg.spin_limit;
   const auto& a0 = fp.st[0].a;
   const int B = a0.B, U = a0.U, strips = fp.st[0].strips;
   const int ips = U * strips;   // items per (stage, slot) = a slot's dependency count
@@ -2348,21 +2189,18 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
   const int per_stage = nbq * ips, total = nst * per_stage;
   int* head = &sy->head[q];
   if (nrx_tid() == 0) {
-    // the first two items in one round trip (a second dependent atomic would add its
-    // latency to every workgroup's start)
-    const int j0 = atomicAdd(head, 2);
-    sh[0] = j0;
-    sh[1] = j0 + 1;
+    // two separate dequeues: with one atomic for both (round 3, d1f0f90) a workgroup's first
+    // two items were consecutive, so a slot's StateInit items all ran as second items and the
+    // first update item of every workgroup found its slot incomplete (1 of 4 update items
+    // un-prefetched)
+    sh[0] = atomicAdd(head, 1);
+    sh[1] = atomicAdd(head, 1);
+    if (fp_arg.dbg_err && blockIdx.x == 0)
+      __hip_atomic_fetch_or(&sy->err, fp_arg.dbg_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   int j = sh[0], jn = sh[1];
   bool have_z = false;   // item j's z image was DMA'd by the previous item's conv3 hook
-  bool pads_zero = false;   // an earlier item zeroed the strip image's pad symbols
-  // NRX_W1_PRE: the next update item's conv1 weights are loaded at the end of the current
-  // item, so their latency overlaps the item-end store drain instead of the next prologue
-  SepStage<kUPD_CINP, kHID> w1n;
-  bool have_w1 = false;
-  int* psig = nullptr;   // NRX_SIG_DEFER: counter of the previous item, not yet added
   auto decode = [&](int jj, int& s, int& b, int& u, int& strip) {
     s = jj / per_stage;
     const int k = jj - s * per_stage;
@@ -2386,13 +2224,13 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
 #endif
     int sn = 0, bn = 0, un = 0, stn = 0;
     if (jn < total) decode(jn, sn, bn, un, stn);
-    // the next item's z image can be prefetched (NRX_FUSED_PREFETCH=0: never; each update
-    // item then loads its own z image at its start)
-    const bool hook = kFusedPrefetch && jn < total && sn >= 1;
-    FusedNext<P> fn{&fp.st[hook ? sn : 0], hook ? done + (sn - 1) * B + bn : nullptr, ips, &sh[2], head, 0, psig};
+    // the next item's z image is prefetched during this item's conv3 epilogue when its inputs
+    // are complete by then (without the prefetch every update item loads its own z image at
+    // its start: -4 %, profiles/r03/ab_fused_prefetch.txt)
+    const bool hook = jn < total && sn >= 1;
+    FusedNext<P> fn{&fp.st[hook ? sn : 0], hook ? done + (sn - 1) * B + bn : nullptr, ips, &sh[2], head, 0};
     const int nfs = stn * P::FO - kHalo;
-    // NRX_DMA_LATE: the body only polls (fn); the DMA goes out after the item (below)
-    const int nb = hook && !kDmaLate ? bn : -1;
+    const int nb = hook ? bn : -1;
     if (s == 0) {
       const auto& a = fp.st[0].a;
       float wm = 1.f;
@@ -2400,38 +2238,20 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
       init_user<P, A2P, 16, TAIL_AGG>(fp.st[0], smem, b, u, strip, wm, true, nb, un, nfs, &fn);
     } else {
       const int fs = strip * P::FO - kHalo;
-      if (!have_z) fused_wait(done + (s - 1) * B + b, ips, sy);
-      const SepStage<kUPD_CINP, kHID>* w1p = kW1Pre && have_w1 ? &w1n : nullptr;
+      if (!have_z) fused_wait(done + (s - 1) * B + b, ips, sy, spin_limit);
       if (s == nst - 1)
-        dma_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn, pads_zero, w1p);
+        dma_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn);
       else
-        dma_item_run<P, CHP, TAIL_AGG>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn, pads_zero, w1p);
+        dma_item_run<P, CHP, TAIL_AGG>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn);
     }
     fstamp(5);
-    have_w1 = kW1Pre && jn < total && sn >= 1;
-    if (have_w1) w1n.load(fp.st[sn].w[0]);
     // item done: every wave's stores have reached L2, then one add on the slot's counter
-    if (!kSigDefer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (nrx_tid() == 0) sh[1] = fn.jnn;
     __syncthreads();
     have_z = hook && sh[2] != 0;
     fstamp(6);
-    psig = nullptr;
-    if (kSigDefer && have_z) {
-      // the next item runs without a dependency wait: its prologue (vmcnt(0) + barrier on
-      // every wave) releases this item's stores and adds the counter
-      psig = done + s * B + b;
-    } else {
-      if (kSigDefer) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-      }
-      if (nrx_tid() == 0) __hip_atomic_fetch_add(done + s * B + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // late DMA: every wave is past the item (barrier above), so the strip image is free; all
-    // eight waves issue the next item's z image, whose prologue waits for it to land
-    if (kDmaLate && have_z) zload_dma_u2<P, 8>(fp.st[sn], X, bn, un, nfs);
-    pads_zero = true;
+    if (nrx_tid() == 0) __hip_atomic_fetch_add(done + s * B + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     j = jn;
     jn = sh[1];
   }
@@ -2454,7 +2274,6 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
   }
 }
 
-#include "nrx_rr.inc"
 
 // ======================================================================= launchers
 
@@ -2638,209 +2457,48 @@ static bool small_strips_fit(const FwdArgs<_Float16, float, _Float16>& a) {
   const long items = (long)a.B * a.U * ((a.F + P::FO - 1) / P::FO);
   return items <= cu_count() && (a.H + 1) * (kHeadSlot + 1024) <= strip_slots<P>() * slot_pitch<P>();
 }
-#ifndef NRX_RR
-#define NRX_RR 1
-#endif
-// NRX_RR in the environment (read at every forward): a bit mask of the launches that take
-// the register-resident kernels -- 1 StateInit, 2 aggregation-tail updates, 4 the readout
-// update.  Default 0 (strip kernels everywhere): measured on the bench shape the RR kernels
-// run 53.5 / 53.5 / 60.6 us against the strip kernels' 43.5 / 45.2 / 35.6 us (same box,
-// profiles/r03/README.md), so they stay an opt-in path, bit-identical to the strip kernels.
-static int rr_mask() {
-  if (NRX_RR == 0) return 0;
-  const char* e = getenv("NRX_RR");
-  return e ? atoi(e) : 0;
-}
-
-// Register-resident path (nrx_rr.inc): throughput tier (more items than CUs), StateInit
-// antenna padding A2P <= 16, U <= 2 (the update z image is an LDS-DMA copy).  The readout
-// launch runs RR when its heads fit BB (one LLR head, 2A <= 16), else the strip kernel's
-// unpaired readout.  Same HBM state layout as the strip kernels: launches mix freely.
-static bool rr_applicable(const FwdArgs<_Float16, float, _Float16>& a, const RrImages* rr) {
-  if (!rr || rr_mask() == 0) return false;
-  const long items = (long)a.B * a.U * ((a.F + PRR::FO - 1) / PRR::FO);
-  return items > cu_count() && 2 * a.A <= 16 && a.U <= 2 && rr->upd[0][0] != nullptr;
-}
-
-// BlockParams of the strip kernels (FO = 24) for one launch of a mixed RR / strip forward
-static BlockParams<P16> strip_params(const BlockParams<PRR>& q, const ModelW<_Float16, float>& W) {
-  BlockParams<P16> bp{};
-  bp.a = q.a;
-  bp.inline_combine = 1;
-  bp.pair = 0;
-  bp.strips = (q.a.F + P16::FO - 1) / P16::FO;
-  bp.norm_pre = q.norm_pre;
-  bp.order_rev = q.order_rev;
-  bp.m = q.m;
-  bp.tail = q.tail;
-  for (int l = 0; l < 3; ++l) bp.w[l] = q.w[l];
-  bp.agg[0] = q.agg[0];
-  bp.agg[1] = q.agg[1];
-  for (int h = 0; h < q.a.H; ++h) {
-    bp.llr[h][0] = W.llr[h][0];
-    bp.llr[h][1] = W.llr[h][1];
+// XCDs (XCCs) of the current device, queried once per device: k_forward keeps one work
+// queue per XCD and needs every XCD to hold the same number of CUs (32 per XCD
+// was assumed)
+static int g_xcc_count[kMaxDevices];
+static int xcc_count() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 0;
+  if (g_xcc_count[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess || n <= 0) n = -1;
+    g_xcc_count[dev] = n;
   }
-  bp.chest[0] = W.chest[0];
-  bp.chest[1] = W.chest[1];
-  return bp;
-}
-
-static hipError_t run_rr(const FwdArgs<_Float16, float, _Float16>& args0, const ModelW<_Float16, float>& W,
-                         const RrImages& rr, int num_it, hipStream_t st, Prof* prof) {
-  const int mask = rr_mask();
-  constexpr int L16 = strip_lds_bytes<P16>();
-  FwdArgs<_Float16, float, _Float16> args = args0;
-  auto B_ = [&](int k) { if (prof) prof->begin(k, st); };
-  auto E_ = [&](int k) { if (prof) prof->end(k, st); };
-  const int strips = (args.F + PRR::FO - 1) / PRR::FO;
-  const int items = args.B * args.U * strips;
-  const int cus = cu_count();
-  RrParams p{};
-  p.bp.a = args;
-  p.bp.inline_combine = 1;
-  p.bp.pair = 0;
-  p.bp.strips = strips;
-  p.items = items;
-  p.per_wg = (items + cus - 1) / cus;
-  int grid = (items + p.per_wg - 1) / p.per_wg;
-  if (grid % 8 && (grid + 7) / 8 * 8 <= cus) grid = (grid + 7) / 8 * 8;   // XCD grouping of work_item
-  for (int h = 0; h < args.H; ++h) {
-    p.bp.llr[h][0] = W.llr[h][0];
-    p.bp.llr[h][1] = W.llr[h][1];
-  }
-  p.bp.chest[0] = W.chest[0];
-  p.bp.chest[1] = W.chest[1];
-  const int nq = args.F * kT * 2 * args.A / 4;
-  p.bp.norm_pre = nq > kNormFusedMaxQ;
-  if (p.bp.norm_pre) {
-    B_(K_NORM);
-    k_norm<<<args.B, 1024, 0, st>>>(args.y, nq, args.norm);
-    E_(K_NORM);
-  }
-  int launch_no = 0;
-  // diagnostic builds: NRX_STAMP_LAUNCH selects the launch that records (-1 - m: StateInit m,
-  // i: update i)
-  auto stamp_sel = [&](int id) {
-#ifdef NRX_STAMPS
-    static const int sel = getenv("NRX_STAMP_LAUNCH") ? atoi(getenv("NRX_STAMP_LAUNCH")) : 0;
-    const int on = sel == id;
-    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_nrx_stamp_on), &on, sizeof(int), 0, hipMemcpyHostToDevice, st);
-    (void)hipStreamSynchronize(st);
-#else
-    (void)id;
-#endif
-  };
-  B_(K_INIT);
-  for (int m = 0; m < args.num_init; ++m) {
-    stamp_sel(-1 - m);
-    for (int l = 0; l < 3; ++l) {
-      p.bp.w[l] = W.init[m][l];
-      p.w_img[l] = rr.init[m][l];
-    }
-    p.bp.m = m;
-    const bool tl = m == args.num_init - 1;
-    p.bp.tail = tl ? TAIL_AGG : TAIL_NONE;
-    p.bp.agg[0] = W.agg[0][0];
-    p.bp.agg[1] = W.agg[0][1];
-    p.tail_img = rr.tail[0];
-    p.tail_bytes = kRrTailBytes;
-    p.bp.order_rev = launch_no++ & 1;
-    if (!(mask & 1)) {
-      BlockParams<P16> bp = strip_params(p.bp, W);
-      const dim3 g16(bp.strips * args.U * args.B);
-      if (2 * args.A <= 8) Launch<P16>::launch_init<8>(g16, L16, st, bp, tl);
-      else Launch<P16>::launch_init<16>(g16, L16, st, bp, tl);
-    } else if (2 * args.A <= 8) {
-      if (tl) k_init_rr<TAIL_AGG, 8><<<grid, 512, kRrLds, st>>>(p);
-      else k_init_rr<TAIL_NONE, 8><<<grid, 512, kRrLds, st>>>(p);
-    } else {
-      if (tl) k_init_rr<TAIL_AGG, 16><<<grid, 512, kRrLds, st>>>(p);
-      else k_init_rr<TAIL_NONE, 16><<<grid, 512, kRrLds, st>>>(p);
-    }
-  }
-  E_(K_INIT);
-  const bool ro_rr = args.H == 1 && rr.heads && rr.heads_bytes <= kRrBBytes;
-  for (int i = 0; i < num_it; ++i) {
-    std::swap(p.bp.a.s_in, p.bp.a.s_out);
-    std::swap(p.bp.a.a, p.bp.a.a_out);
-    for (int l = 0; l < 3; ++l) {
-      p.bp.w[l] = W.upd[i][l];
-      p.w_img[l] = rr.upd[i][l];
-    }
-    const bool last = i == num_it - 1;
-    p.bp.order_rev = launch_no++ & 1;
-    stamp_sel(i);
-    B_(K_UPDATE);
-    if (!last) {
-      p.bp.tail = TAIL_AGG;
-      p.bp.agg[0] = W.agg[i + 1][0];
-      p.bp.agg[1] = W.agg[i + 1][1];
-      p.tail_img = rr.tail[i + 1];
-      p.tail_bytes = kRrTailBytes;
-      if (mask & 2) {
-        k_update_rr<TAIL_AGG><<<grid, 512, kRrLds, st>>>(p);
-      } else {
-        BlockParams<P16> bp = strip_params(p.bp, W);
-        k_update<P16, 16, TAIL_AGG><<<dim3(bp.strips * args.U * args.B), 512, L16, st>>>(bp);
-      }
-    } else if (ro_rr && (mask & 4)) {
-      p.bp.tail = TAIL_READOUT_WB;
-      p.tail_img = rr.heads;
-      p.tail_bytes = rr.heads_bytes;
-      k_update_rr<TAIL_READOUT_WB><<<grid, 512, kRrLds, st>>>(p);
-    } else {
-      // strip kernel readout (several LLR heads, or heads wider than BB)
-      p.bp.tail = TAIL_READOUT;
-      BlockParams<P16> bp = strip_params(p.bp, W);
-      const dim3 g16(bp.strips * args.U * args.B);
-      constexpr int L = L16;
-      k_update<P16, 16, TAIL_READOUT><<<g16, 512, L, st>>>(bp);
-    }
-    E_(K_UPDATE);
-  }
-  return hipGetLastError();
-}
-
-#ifndef NRX_FUSED_SMALL
-#define NRX_FUSED_SMALL 0
-#endif
-// NRX_FUSED_SMALL=1 (build flag): the small-grid tiers (batch-1 latency) through k_forward as
-// well.  Measured slower (profiles/r03/ab_fused_small_latency.txt): a slot's items all sit on
-// one XCD's queue (the hand-offs stay inside one L2), so a 132-PRB slot runs on 32 CUs
-// instead of 256 (0.093 -> 0.397 ms), and at 4 PRB the dependency waits and un-prefetched
-// z-loads cost more than the two launch boundaries they remove (0.057 -> 0.067 ms).
-constexpr bool kFusedSmall = NRX_FUSED_SMALL != 0;
-
-// NRX_FUSED=0 in the environment (read at every forward) takes the three-launch forward
-// instead of k_forward (A/B and bit-identity tests).
-static bool fused_enabled() {
-  const char* e = getenv("NRX_FUSED");
-  return !e || atoi(e) != 0;
+  return g_xcc_count[dev];
 }
 
 // k_forward covers the bench-type models: U <= 2 (z images are LDS-DMA copies), one StateInit
-// (no Var-IO mix), one LLR head whose readout fits the paired-readout WB layout, 2A <= 16.
-// 24-row strips (throughput tier) need at least two items per CU; the small-grid tiers
-// (8 / 16-row strips, no more items than CUs) take it whatever the count: there it removes
-// the two launch boundaries from a batch-1 forward.
+// (no Var-IO mix), one LLR head whose readout fits the paired-readout WB layout, 2A <= 16, at
+// most kFusedMaxStages - 1 iterations; 24-row strips with at least two items per CU (the
+// small-grid tiers keep the three launches: through k_forward they were slower for batch-1
+// latency, profiles/r03/ab_fused_small_latency.txt); a device whose XCDs hold equal CU counts
+// (1..8 XCDs, the queue is picked by the hardware XCC id).
 template <class P>
-static bool fused_applicable(const FwdArgs<_Float16, float, _Float16>& a, int num_it, const void* sync) {
-  if (!sync || !fused_enabled()) return false;
+static bool fused_applicable(const FwdArgs<_Float16, float, _Float16>& a, int num_it, const FusedCtl& fc) {
+  if (!fc.sync || !fc.enabled) return false;
+  const int cus = cu_count(), nx = xcc_count();
+  if (nx < 1 || nx > 8 || cus % nx != 0) return false;
   const long items = (long)a.B * a.U * ((a.F + P::FO - 1) / P::FO);
-  const bool tier = P::FO != P16::FO || items >= 2L * cu_count();
-  return tier && a.U <= 2 && a.num_init == 1 && a.H == 1 && 1 + num_it <= kFusedMaxStages && 2 * a.A <= 16 &&
-         a.B <= kFusedMaxB && heads_fit_wb(a.bits_max, 16, 2 * a.A) &&
+  return items >= 2L * cus && a.U <= 2 && a.num_init == 1 && a.H == 1 && 1 + num_it <= kFusedMaxStages &&
+         2 * a.A <= 16 && a.B <= kFusedMaxB && heads_fit_wb(a.bits_max, 16, 2 * a.A) &&
          strip_slots<P>() * slot_pitch<P>() + kHW2 + 256 * (a.bits_max + 16) <= fused_lds<P>();
 }
 
 template <class P>
 static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, const ModelW<_Float16, float>& W,
-                            int num_it, hipStream_t st, Prof* prof, void* sync) {
+                            int num_it, hipStream_t st, Prof* prof, const FusedCtl& fc) {
   FusedParams<P> fp{};
-  fp.sync = reinterpret_cast<FusedSync*>(sync);
+  fp.sync = reinterpret_cast<FusedSync*>(fc.sync);
   fp.nst = 1 + num_it;
   const int cus = cu_count();
-  fp.nq = cus / 32 < 1 ? 1 : (cus / 32 > 8 ? 8 : cus / 32);   // MI355X: 8 XCDs x 32 CUs
+  fp.nq = xcc_count();
+  fp.spin_limit = fc.spin_limit;
+  fp.dbg_err = fc.dbg_err;
   const int nq = args.F * kT * 2 * args.A / 4;
   const bool norm_pre = nq > kNormFusedMaxQ;
   auto B_ = [&](int k) { if (prof) prof->begin(k, st); };
@@ -2900,33 +2558,33 @@ static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, cons
 }
 
 hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args,
-                              const ModelW<_Float16, float>& W, const RrImages* rr, int num_it, hipStream_t st,
-                              Prof* prof, void* fused_sync) {
+                              const ModelW<_Float16, float>& W, int num_it, hipStream_t st,
+                              Prof* prof, const FusedCtl& fc) {
   if (NRX_SMALL_STRIPS != 0) {
-    if (small_strips_fit<P16S>(args)) {
-      if constexpr (kFusedSmall)
-        if (fused_applicable<P16S>(args, num_it, fused_sync)) return run_fused<P16S>(args, W, num_it, st, prof, fused_sync);
-      return Launch<P16S>::run(args, W, num_it, st, prof);
-    }
-    if (small_strips_fit<P16M>(args)) {
-      if constexpr (kFusedSmall)
-        if (fused_applicable<P16M>(args, num_it, fused_sync)) return run_fused<P16M>(args, W, num_it, st, prof, fused_sync);
-      return Launch<P16M>::run(args, W, num_it, st, prof);
-    }
+    if (small_strips_fit<P16S>(args)) return Launch<P16S>::run(args, W, num_it, st, prof);
+    if (small_strips_fit<P16M>(args)) return Launch<P16M>::run(args, W, num_it, st, prof);
   }
-  if (rr_applicable(args, rr)) return run_rr(args, W, *rr, num_it, st, prof);
-  if (fused_applicable<P16>(args, num_it, fused_sync)) return run_fused<P16>(args, W, num_it, st, prof, fused_sync);
+  if (fused_applicable<P16>(args, num_it, fc)) return run_fused<P16>(args, W, num_it, st, prof, fc);
   return Launch<P16>::run(args, W, num_it, st, prof);
+}
+
+bool fused_would_run(const FwdArgs<_Float16, float, _Float16>& args, int num_it, const FusedCtl& fc) {
+  if (NRX_SMALL_STRIPS != 0 && (small_strips_fit<P16S>(args) || small_strips_fit<P16M>(args))) return false;
+  return fused_applicable<P16>(args, num_it, fc);
 }
 
 size_t fused_sync_bytes() { return kFusedSyncBytes; }
 
-// {error word, items that waited, polls} of the fused forward since the last reset
-// (blocking read; reset clears the three words)
-hipError_t fused_sync_status(void* sync, int* st, bool reset) {
+// {error word, items that waited, polls} of the fused forward since the last reset.  Blocking:
+// the stream the forwards ran on is synchronised first, so the read and the reset never race
+// with a k_forward in flight; reset clears the three words.
+hipError_t fused_sync_status(void* sync, int* st, bool reset, hipStream_t stream) {
   FusedSync* sy = reinterpret_cast<FusedSync*>(sync);
-  hipError_t e = hipMemcpy(st, &sy->err, 3 * sizeof(int), hipMemcpyDeviceToHost);
+  hipError_t e = hipStreamSynchronize(stream);
+  if (e != hipSuccess) e = hipDeviceSynchronize();   // that stream is gone: wait for everything
+  if (e == hipSuccess) e = hipMemcpy(st, &sy->err, 3 * sizeof(int), hipMemcpyDeviceToHost);
   if (e == hipSuccess && reset) e = hipMemset(&sy->err, 0, 3 * sizeof(int));
+  if (e == hipSuccess && reset) e = hipDeviceSynchronize();
   return e;
 }
 
@@ -2938,18 +2596,10 @@ hipError_t launch_forward_f64(const FwdArgs<double, double, float>& args,
 
 hipError_t setup_kernels() {
   (void)cu_count();
+  (void)xcc_count();
   hipError_t e = Launch<P16>::setup();
   hipError_t e1 = Launch<P16S>::setup();
   if (e1 == hipSuccess) e1 = Launch<P16M>::setup();
-  if (e1 == hipSuccess) {
-    const void* fs[] = {(const void*)k_init_rr<TAIL_AGG, 8>, (const void*)k_init_rr<TAIL_NONE, 8>,
-                        (const void*)k_init_rr<TAIL_AGG, 16>, (const void*)k_init_rr<TAIL_NONE, 16>,
-                        (const void*)k_update_rr<TAIL_AGG>, (const void*)k_update_rr<TAIL_READOUT_WB>};
-    for (const void* f : fs) {
-      hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kRrLds);
-      if (r != hipSuccess) e1 = r;
-    }
-  }
   hipError_t e2 = Launch<P64>::setup();
   auto set_fused = [&](const void* f, int lds) {
     hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -2957,12 +2607,6 @@ hipError_t setup_kernels() {
   };
   set_fused((const void*)k_forward<P16, 8, 16>, fused_lds<P16>());
   set_fused((const void*)k_forward<P16, 16, 16>, fused_lds<P16>());
-  if constexpr (kFusedSmall) {
-    set_fused((const void*)k_forward<P16S, 8, 16>, fused_lds<P16S>());
-    set_fused((const void*)k_forward<P16S, 16, 16>, fused_lds<P16S>());
-    set_fused((const void*)k_forward<P16M, 8, 16>, fused_lds<P16M>());
-    set_fused((const void*)k_forward<P16M, 16, 16>, fused_lds<P16M>());
-  }
   return e != hipSuccess ? e : (e1 != hipSuccess ? e1 : e2);
 }
 
@@ -2972,7 +2616,7 @@ int strip_width(int precision) { return precision == 0 ? P16::FO : P64::FO; }
 extern "C" int nrx_debug_stamps(void* out, int n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nrx_stamps), (size_t)n * 64 * 8, 0, hipMemcpyDeviceToHost);
 }
-extern "C" int nrx_debug_rr_stamps(void* out, int n) {
+extern "C" int nrx_debug_fused_stamps(void* out, int n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nrx_rr_stamps), (size_t)n * 64 * 8, 0, hipMemcpyDeviceToHost);
 }
 #endif

@@ -90,6 +90,9 @@ def sim_ber(engine: CGNNEngine, gen: SlotGenerator, ebno_dbs: Sequence[float], b
             it += 1
             if it % sync_every and it < max_mc_iter:
                 continue
+            # the one-launch forward's error word: a timed-out or incomplete forward raises here
+            # instead of entering the counts (include/nrx.h nrx_fused_status)
+            engine.check()
             tot = counts.sum(0)
             if host_reduce:
                 tot = tot.cpu()

@@ -93,6 +93,22 @@ def io_bytes_per_slot(spec: ModelSpec, num_tx: int, num_subcarriers: int, elem: 
     return {"in": inp, "out": out}
 
 
+def compulsory_bytes_per_forward(spec: ModelSpec, batch: int, num_tx: int, num_subcarriers: int,
+                                 with_h: bool = True) -> int:
+    """SURVEY.md 8(d) compulsory HBM bytes of one forward over ``batch`` slots, as the C ABI
+    takes and returns them (f32): y ``[B,F,14,2A]`` and h_hat ``[B,U,F,14,2A]`` in, the f32
+    LLRs of every head and (with_h) h_ref ``[B,U,F,14,2A]`` out, pe ``[U,F,14,2]`` once (shared
+    by the slots).  cfg2 (B 128, 2 UE, 4 PRB): 16.5 MB."""
+    re = num_subcarriers * 14
+    a2 = 2 * spec.num_rx_ant
+    y = batch * re * a2 * 4
+    h = batch * num_tx * re * a2 * 4 if spec.use_h_hat else 0
+    pe = num_tx * re * 2 * 4
+    llr = batch * num_tx * re * spec.bits_max * 4 * spec.num_llr_heads
+    h_ref = batch * num_tx * re * a2 * 4 if with_h else 0
+    return y + h + pe + llr + h_ref
+
+
 def update_launch_split_per_re_user(spec: ModelSpec, num_it: int) -> dict:
     """The k_update launch's algorithmic FLOPs split by the pipe that executes them:
     the depthwise 3x3 taps run on the VALU (packed f16 FMAs), everything else (pointwise

@@ -94,12 +94,29 @@ class CGNNEngine:
     def fused_status(self, reset: bool = False, full: bool = False):
         """One-launch forward counters since the last reset: the sticky error bits (1: a
         dependency wait timed out, 2: items left undone), or with ``full`` the dict
-        {error, waited, polls} (update items that could not be prefetched, and their polls)."""
+        {error, waited, polls} (update items that could not be prefetched, and their polls).
+        Reads, never raises on the error bits (``check`` does)."""
         st = (ctypes.c_int32 * 3)()
-        _lib.check(self._lib.nrx_fused_status(self._h, st, int(reset)))
+        rc = self._lib.nrx_fused_status(self._h, st, int(reset))
+        if rc != _lib.NRX_ERR_FUSED:
+            _lib.check(rc)
         if full:
             return {"error": st[0], "waited": st[1], "polls": st[2]}
         return st[0]
+
+    def check(self):
+        """Raise ``NRXError`` (code NRX_ERR_FUSED) if a one-launch forward since the last check
+        reported an error -- its LLRs are invalid (include/nrx.h nrx_fused_status).  Blocking
+        (synchronises the stream of the last forward); clears the counters."""
+        st = (ctypes.c_int32 * 3)()
+        _lib.check(self._lib.nrx_fused_status(self._h, st, 1))
+
+    def fused_config(self, enable: Optional[bool] = None, spin_limit: int = 0, inject_err: int = 0):
+        """One-launch forward control (include/nrx.h nrx_fused_config): ``enable`` True/False
+        (None: unchanged), the dependency-wait bound (<= 0: default) and error bits to inject
+        (test hook)."""
+        en = -1 if enable is None else int(bool(enable))
+        _lib.check(self._lib.nrx_fused_config(self._h, en, int(spin_limit), int(inject_err)))
 
     def profile_read(self):
         """{kernel: (launches, total_ms)} since the last profile(True)."""
@@ -358,6 +375,10 @@ class CGNN:
 
     __call__ = forward
 
+    def check(self):
+        """Raise if a one-launch forward since the last check reported an error."""
+        self.engine.check()
+
 
 class NeuralReceiver:
     """Drop-in receiver: rx grid + PE + active DMRS ports (+ h_hat) -> LLRs."""
@@ -385,6 +406,11 @@ class NeuralReceiver:
     @num_it.setter
     def num_it(self, val):
         self.cgnn.num_it = val
+
+    def check(self):
+        """Raise ``NRXError`` if a one-launch forward since the last check reported an error
+        (its outputs are invalid); blocking."""
+        self.cgnn.check()
 
     def positional_encoding(self, num_tx: int, num_subcarriers: int):
         torch = _torch()
@@ -433,7 +459,7 @@ class NeuralReceiver:
             # CGNNOFDM.forward: y [B,1,A,T,F] complex -> [B,F,T,2A] (neural_rx.py:831-833),
             # done by libnrx (nrx_forward_ex, NRX_Y_SIONNA_RG)
             y, y_layout = rx_grid, "sionna"
-            if not y.is_complex():
+            if y.dtype != torch.complex64:   # real or complex128 grids
                 y = y.to(torch.complex64)
             B, F = y.shape[0], y.shape[4]
         elif layout == "aerial":

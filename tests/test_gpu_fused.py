@@ -2,18 +2,18 @@
 
 k_forward runs the same per-item code as k_init / k_update, only scheduled through per-XCD
 work queues with cross-workgroup dependency counters, so its outputs
-must equal the three-launch path bit for bit (NRX_FUSED=0 selects that path at every
-forward).  The oracle comparison of the same launch shape is tests/test_gpu_baseline_shapes.py
+must equal the three-launch path bit for bit (``fused_config(enable=False)`` selects that
+path per handle).  The oracle comparison of the same launch shape is tests/test_gpu_baseline_shapes.py
 (cfg2, B = 128, which takes k_forward by default).  Covered here: the bench shape, inactive
 users, U = 1, num_it = 1 (StateInit straight into the readout stage), repeated forwards (the
-counters are reset by the last workgroup of each launch), a hipGraph replay, and the sticky
-timeout word staying 0.
+counters are reset by the last workgroup of each launch), a hipGraph replay, the sticky
+timeout word staying 0, that an error word reaches the caller (CGNNEngine.check, sim_ber) and
+that a second stream is refused while the first still runs.
 """
-import os
-
 import numpy as np
 import pytest
 
+from neural_rx_amd._lib import NRX_ERR_FUSED, NRXError
 from tests.helpers import make_case, run_engine
 from tests.test_gpu_parity import engine_for
 
@@ -21,15 +21,12 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(case, fused: bool):
-    old = os.environ.get("NRX_FUSED")
-    os.environ["NRX_FUSED"] = "1" if fused else "0"
+    eng = engine_for(case)
+    eng.fused_config(enable=fused)
     try:
-        return run_engine(case, "f16", engine_for(case))
+        return run_engine(case, "f16", eng)
     finally:
-        if old is None:
-            del os.environ["NRX_FUSED"]
-        else:
-            os.environ["NRX_FUSED"] = old
+        eng.fused_config(enable=True)
 
 
 def _took_fused(case) -> bool:
@@ -85,8 +82,8 @@ def test_fused_graph_replay():
     dev = "cuda:0"
     t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
     args = (t(case.y), t(case.pe), t(case.h_hat), t(case.active), t(case.mcs_mask))
-    os.environ["NRX_FUSED"] = "1"
-    try:
+    eng.fused_config(enable=True)
+    if True:
         st = torch.cuda.Stream()
         with torch.cuda.stream(st):
             eng.forward(*args, num_it=None, precision="f16")    # warm-up (workspace allocation)
@@ -97,8 +94,72 @@ def test_fused_graph_replay():
         for _ in range(3):
             g.replay()
         torch.cuda.synchronize()
-    finally:
-        del os.environ["NRX_FUSED"]
     assert np.array_equal(ref["llr_raw"], llr.cpu().numpy())
     assert eng.fused_status(reset=True) == 0
+
+
+def _device_args(case):
+    import torch
+    t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a, np.float32)).to("cuda:0")  # noqa: E731
+    return (t(case.y), t(case.pe), t(case.h_hat), t(case.active), t(case.mcs_mask))
+
+
+def test_fused_error_reaches_caller():
+    """An error word set in the one-launch forward (injected through the test hook) is raised
+    by CGNNEngine.check / NeuralReceiver.check as NRX_ERR_FUSED, not returned as NRX_OK LLRs."""
+    case = make_case("nrx_rt", batch=128, users=2, prbs=4, snr_db=12, seed=37)
+    eng = engine_for(case)
+    eng.check()                                   # clean before
+    args = _device_args(case)
+    eng.fused_config(inject_err=4)
+    try:
+        eng.forward(*args, num_it=None, precision="f16")
+        with pytest.raises(NRXError) as ei:
+            eng.check()
+        assert ei.value.code == NRX_ERR_FUSED
+    finally:
+        eng.fused_config(inject_err=0)
+    eng.forward(*args, num_it=None, precision="f16")
+    eng.check()                                   # cleared by the failed check, clean again
+
+
+def test_fused_error_raised_by_sim_ber():
+    """sim_ber checks the error word at every reduction window."""
+    from neural_rx_amd import weights as W
+    from neural_rx_amd.config import get_config, spec_from_config
+    from neural_rx_amd.evaluate import sim_ber
+    from neural_rx_amd.generator import GenParams, SlotGenerator
+    from neural_rx_amd.receiver import CGNNEngine
+    cfg = get_config("nrx_rt")
+    eng = CGNNEngine(spec_from_config(cfg), W.load(cfg.label), 0)
+    gen = SlotGenerator(GenParams.from_config(cfg, num_tx=2, num_prbs=4), device=0)
+    ok = sim_ber(eng, gen, [8.0], batch_size=128, max_mc_iter=2, num_target_block_errors=10 ** 9, sync_every=2)
+    assert ok.slots == 256
+    eng.fused_config(inject_err=2)
+    with pytest.raises(NRXError):
+        sim_ber(eng, gen, [8.0], batch_size=128, max_mc_iter=2, num_target_block_errors=10 ** 9, sync_every=2)
+    eng.close()
+
+
+def test_fused_second_stream_refused_while_busy():
+    """One stream per handle on the one-launch path: a forward on another stream is refused
+    (NRX_ERR_BUSY) while the previous forward's stream still has work; accepted once idle."""
+    import torch
+    from neural_rx_amd._lib import NRX_ERR_BUSY
+    case = make_case("nrx_rt", batch=128, users=2, prbs=4, snr_db=12, seed=38)
+    eng = engine_for(case)
+    args = _device_args(case)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    with torch.cuda.stream(s1):
+        eng.forward(*args, num_it=None, precision="f16")
+        torch.cuda._sleep(50_000_000)             # keep s1 busy (spin kernel)
+    with torch.cuda.stream(s2):
+        with pytest.raises(NRXError) as ei:
+            eng.forward(*args, num_it=None, precision="f16")
+    assert ei.value.code == NRX_ERR_BUSY
+    s1.synchronize()
+    with torch.cuda.stream(s2):
+        eng.forward(*args, num_it=None, precision="f16")
+    torch.cuda.synchronize()
+    eng.check()
 

@@ -21,7 +21,7 @@ from neural_rx_amd.config import get_config, spec_from_config  # noqa: E402
 from neural_rx_amd.receiver import CGNNEngine, compute_pe  # noqa: E402
 
 lib = _lib.load(LIB)
-lib.nrx_debug_rr_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+lib.nrx_debug_fused_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 cfg = get_config("nrx_rt")
 spec = spec_from_config(cfg)
 B, U = int(os.environ.get("NRX_STAMP_B", 128)), 2
@@ -35,7 +35,7 @@ for _ in range(300):
 torch.cuda.synchronize()
 n = 256
 buf = np.zeros((n, 64), np.uint64)
-lib.nrx_debug_rr_stamps(buf.ctypes.data, n)
+lib.nrx_debug_fused_stamps(buf.ctypes.data, n)
 buf = buf.astype(np.int64).reshape(n, 8, 8)
 t0 = buf[:, 0, 0].min()
 names = ["prologue", "conv1", "conv2", "conv3", "epilogue", "signal"]
