@@ -206,13 +206,15 @@ int build_model(const nrx_desc* d, const float* const* w, int kc, DeviceModel<WT
   DO ch[2];
   const int icin = init_cin(d);
   // StateInit input z = [y (2A), pe (2), h (2A)] (copy_pytorch.py:175-183) is laid out
-  // with each antenna block padded to A2P = init_a2p(A): y at [0, 2A), pe at A2P, A2P+1,
-  // h at [A2P+2, A2P+2+2A); the padded channels carry zero weights.
+  // with each antenna block padded to A2P = init_a2p(A): y at [0, 2A), h at [A2P, A2P+2A),
+  // pe at 2 A2P, 2 A2P + 1 (so that an 8-channel lane chunk is all y, all h or pe: the
+  // one-launch forward's conv1 loads them straight from y / h_hat / pe); the padded channels
+  // carry zero weights.
   const int a2p = init_a2p(d->num_rx_ant);
   std::vector<int> ipos(icin);
   for (int c = 0; c < icin; ++c) {
     const int a2 = 2 * d->num_rx_ant;
-    ipos[c] = c < a2 ? c : (c < a2 + 2 ? a2p + (c - a2) : a2p + 2 + (c - a2 - 2));
+    ipos[c] = c < a2 ? c : (c < a2 + 2 ? 2 * a2p + (c - a2) : a2p + (c - a2 - 2));
   }
   const int icinp = pow2_at_least(round_up(2 * a2p + 2, kc), 32);
   out->init_cinp = icinp;
@@ -360,6 +362,10 @@ static size_t state_bytes(const nrx_shape* s, int precision) {
   const size_t es = precision == NRX_PREC_F16 ? 2 : 4;
   return align256((size_t)s->batch * s->num_tx * s->num_subcarriers * kT * kDS * es);
 }
+// pe16 plane [U][F][14][56] f16 of the one-launch forward (f16 workspaces only)
+static size_t pe16_bytes(const nrx_shape* s, int precision) {
+  return precision == NRX_PREC_F16 ? align256((size_t)s->num_tx * s->num_subcarriers * kT * kDS * 2) : 0;
+}
 
 static int check_shape(const nrx_shape* s) {
   if (!s) return fail(NRX_ERR_INVALID_ARG, "shape is NULL");
@@ -403,6 +409,11 @@ static void fill_args(FwdArgs<WT, BT, S>& a, const nrx_handle* h, const nrx_io* 
   a.s_out = (S*)p;
   a.a = (S*)(p + 3 * sb);
   a.a_out = (S*)(p + 2 * sb);
+  a.ws_base = (const char*)ws;
+  const size_t pb = pe16_bytes(s, io->precision);
+  a.pe16 = pb ? (S*)(p + 4 * sb) : nullptr;
+  const size_t total = (size_t)(p + 4 * sb + pb - (char*)ws);
+  a.ws_bytes = total < 0xFFFFFFFFull ? (unsigned)total : 0xFFFFFFFFu;
 }
 
 
@@ -479,7 +490,8 @@ int nrx_workspace_size(const nrx_handle* h, const nrx_shape* shape, int32_t prec
   if (rc) return rc;
   if (precision != NRX_PREC_F16 && precision != NRX_PREC_F32X)
     return fail(NRX_ERR_INVALID_ARG, "unknown precision");
-  *bytes = align256((size_t)shape->batch * sizeof(double)) + 4 * state_bytes(shape, precision);
+  *bytes = align256((size_t)shape->batch * sizeof(double)) + 4 * state_bytes(shape, precision) +
+           pe16_bytes(shape, precision);
   return NRX_OK;
 }
 

@@ -98,6 +98,12 @@ struct FwdArgs {
   S* s_out;
   S* a;                            // aggregate read by this update
   S* a_out;                        // aggregate written by the tail
+  // one-launch forward (f16): the workspace as one buffer resource for conv1's z rows, and
+  // the pe16 plane [U][F][14][56] (pe as f16 in channels 0, 1 of each 8-channel chunk 0;
+  // written by the StateInit items, read as z chunk 14 by the update items' conv1)
+  const char* ws_base;
+  unsigned ws_bytes;
+  S* pe16;
 };
 
 // The one-launch forward's control block (nrx_api.cpp fills it from the handle): the

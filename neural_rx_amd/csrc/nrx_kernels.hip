@@ -307,6 +307,33 @@ __device__ __forceinline__ void lds_store(char* base, int off, typename P::Real 
   *reinterpret_cast<typename P::S*>(base + off) = (typename P::S)v;
 }
 
+// ------------------------------------------------ z rows straight from memory
+// The z image of a k_forward update item, [a | s | pe] = chunks [0, 7) of the other user's
+// act*sp plane, [7, 14) of the own state plane and chunk 14 of the pe16 plane (pe as f16,
+// zero-padded to 8 channels), read by conv1 straight from L2 / HBM into its depthwise
+// registers with buffer loads instead of being staged in the LDS strip image.  One buffer
+// resource spans the workspace; lane (t, g) keeps, per K chunk kc, the byte offset of its
+// 16-byte chunk q = 4 kc + g in grid row 0 (kGzOob for zero chunks: pad symbols, q = 15, the
+// missing other user of U = 1), and a grid row adds f * kGzRow as the wave-uniform soffset
+// (kGzOob for rows outside the grid).  Out-of-range buffer loads return zeros.
+constexpr unsigned kGzOob = 0x40000000u;          // > any workspace this path is taken for
+constexpr unsigned kGzRow = kT * kDS * 2;          // bytes per grid row of a state plane
+struct GZ {
+  __amdgpu_buffer_rsrc_t rsrc;
+  unsigned off[4];   // per K chunk
+  int f_start, F;
+  half8 x0[6];       // K chunk 0 of the wave's R + 2 input rows, loaded in the item prologue
+  __device__ unsigned row_soff(int slot) const {
+    const int f = f_start + slot;
+    return (f >= 0 && f < F) ? (unsigned)f * kGzRow : kGzOob;
+  }
+  __device__ half8 load(int kc, unsigned soff) const {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off[kc], (int)soff, 0);
+    return __builtin_bit_cast(half8, v);
+  }
+};
+
 // ------------------------------------------------ depthwise 3x3 + pointwise on MFMA
 // Strip image in LDS: slot (one subcarrier row) x 16 symbols x up to 128 channels, with a
 // fixed slot pitch so that every layer of a block can run in place in one buffer.
@@ -483,10 +510,10 @@ __device__ __forceinline__ void conv_chunk(const char* X, const int (&rb)[R + 2]
   }
 }
 
-template <class P, int CINP, int COUTP, int R, class WS>
+template <class P, int CINP, int COUTP, int R, class WS, bool GZIN = false>
 __device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int t, int g, int lane,
                                           const WS& ws,
-                                          typename P::Acc (&acc)[R][COUTP / 16]) {
+                                          typename P::Acc (&acc)[R][COUTP / 16], const GZ* gz = nullptr) {
   constexpr int NQ = CINP * (int)sizeof(typename P::S) / 16;
   constexpr int NKC = CINP / P::KC;
   const int sw = swz<NQ>(t);
@@ -513,10 +540,23 @@ __device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int
     using DV = typename P::DV;
     constexpr int NT = COUTP / 16;
     DV xs[R + 2], w[9];
-    auto load = [&](int kc) {
-      const int off = ((kc * 4 + g) ^ sw) * 16;
+    unsigned soff[R + 2];
+    if constexpr (GZIN) {
 #pragma unroll
-      for (int i = 0; i < R + 2; ++i) xs[i] = P::ld_lds(X + rb[i] + off);
+      for (int i = 0; i < R + 2; ++i) soff[i] = gz->row_soff(s0 - 1 + i);
+    }
+    auto load = [&](int kc) {
+      if constexpr (GZIN) {
+        static_assert(sizeof(typename P::S) == 2 && (CINP == 128 || CINP == 32) && R + 2 <= 6,
+                      "global z rows: f16 update conv1 / StateInit conv1 (one preloaded chunk)");
+        // chunk 0 was issued in the item prologue (its latency behind the conv1-weight staging)
+#pragma unroll
+        for (int i = 0; i < R + 2; ++i) xs[i] = kc == 0 ? gz->x0[i] : gz->load(kc, soff[i]);
+      } else {
+        const int off = ((kc * 4 + g) ^ sw) * 16;
+#pragma unroll
+        for (int i = 0; i < R + 2; ++i) xs[i] = P::ld_lds(X + rb[i] + off);
+      }
       ws.dw_taps(kc, g, w);
     };
     load(0);
@@ -553,9 +593,9 @@ __device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int
 // overwrite input slots of rows this round consumed (in-place layers: the output of
 // position p goes to slot p - in_off - 1, which no later round reads).  All waves execute
 // the same barriers.
-template <class P, int CINP, int COUTP, int R, class WS, class Epi, class Post>
+template <class P, int CINP, int COUTP, int R, bool GZIN, class WS, class Epi, class Post>
 __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off, int p0, bool act, bool first_round,
-                                           const WS& ws, Epi& epi, Post& post_math) {
+                                           const WS& ws, Epi& epi, Post& post_math, const GZ* gz) {
   using E = std::decay_t<Epi>;
   const int lane = nrx_tid() & 63;
   const int t = lane & 15, g = lane >> 4;
@@ -570,7 +610,7 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
 #pragma unroll
         for (int n = 0; n < COUTP / 16; ++n) acc[r][n] = ws.bias_acc(n, g);
     } else {
-      conv_rows<P, CINP, COUTP, R>(X, p0 - in_off, nslots, t, g, lane, ws, acc);
+      conv_rows<P, CINP, COUTP, R, WS, GZIN>(X, p0 - in_off, nslots, t, g, lane, ws, acc, gz);
     }
   }
   stamp(9 + 5 * in_off);
@@ -629,9 +669,10 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
 // split 4 / 3 per wave so that the 4 SIMDs (waves w and w + 4 share one) carry equal row
 // counts (28 rows: 7 per SIMD; 26: 7,7,6,6; 24: 6 each) instead of whole waves idling.
 // f64 policy: rounds of 8 waves x P::R rows.
-template <class P, int CINP, int COUTP, class WS, class Epi, class Post>
+template <class P, int CINP, int COUTP, bool GZIN = false, class WS, class Epi, class Post>
 __device__ __forceinline__ void conv_layer(const char* X, int nslots, int in_off, int pos_lo,
-                                           int pos_hi, const WS& ws, Epi&& epi, Post&& post_math) {
+                                           int pos_hi, const WS& ws, Epi&& epi, Post&& post_math,
+                                           const GZ* gz = nullptr) {
   const int wave = __builtin_amdgcn_readfirstlane(nrx_tid() >> 6);
   if constexpr (P::WLDS) {
     static_assert(P::R == 4, "f16 row split assumes passes of 4 / 3 rows");
@@ -640,12 +681,13 @@ __device__ __forceinline__ void conv_layer(const char* X, int nslots, int in_off
     n4 = n4 < 0 ? 0 : n4;
     const int p0 = pos_lo + 4 * (wave < n4 ? wave : n4) + 3 * (wave > n4 ? wave - n4 : 0);
     const bool act = p0 < pos_hi;
-    if (wave < n4) layer_pass<P, CINP, COUTP, 4>(X, nslots, in_off, p0, act, true, ws, epi, post_math);
-    else layer_pass<P, CINP, COUTP, 3>(X, nslots, in_off, p0, act, true, ws, epi, post_math);
+    if (wave < n4) layer_pass<P, CINP, COUTP, 4, GZIN>(X, nslots, in_off, p0, act, true, ws, epi, post_math, gz);
+    else layer_pass<P, CINP, COUTP, 3, GZIN>(X, nslots, in_off, p0, act, true, ws, epi, post_math, gz);
   } else {
     for (int base = pos_lo; base < pos_hi; base += 8 * P::R) {
       const int p0 = base + wave * P::R;
-      layer_pass<P, CINP, COUTP, P::R>(X, nslots, in_off, p0, p0 < pos_hi, base == pos_lo, ws, epi, post_math);
+      layer_pass<P, CINP, COUTP, P::R, false>(X, nslots, in_off, p0, p0 < pos_hi, base == pos_lo, ws, epi, post_math,
+                                              nullptr);
     }
   }
 }
@@ -655,14 +697,16 @@ struct NoPref {};
 // In-place epilogue: ReLU, zero outside the grid, store to slot p-in_off-1.  Lanes
 // t >= 14 do not store: the pad symbols of every slot are zero from the start of the
 // block and stay zero (P16); P64 writes them as zeros.
-template <class P, int COUTP, class WS>
+// ER: the first row written before the layer barrier (rows 0, 1 of a wave land in slots the
+// previous wave may still read; 0 when the layer's input is not in the image: GZ conv1).
+template <class P, int COUTP, class WS, int ER = 2>
 struct EpiInPlace {
   template <int R>
   using PrefT = NoPref;
   static constexpr bool kNoBarrier = false;
   static constexpr bool kNextHook = false;
   static constexpr bool kNextHookRO = false;
-  static constexpr int kEarlyRow = 2;
+  static constexpr int kEarlyRow = ER;
   char* X;
   int in_off, pos_hi, f_start, F;
   WS ws;
@@ -836,13 +880,14 @@ __device__ __forceinline__ size_t srow(int b, int u, int f, int t, int U, int F)
 
 // Runs one separable layer of a block over the strip.  P16: the layer's weights are
 // already in the LDS image WB (staged by the previous phase); `post` runs after the math.
-template <class P, int CINP, int COUTP, class Epi, class Post>
+template <class P, int CINP, int COUTP, bool GZIN = false, class Epi, class Post>
 __device__ __forceinline__ void run_layer(char* X, char* WB, const SepW<typename P::WT, typename P::BT>& w,
-                                          int in_off, int pos_lo, int pos_hi, Epi&& epi_of, Post&& post) {
+                                          int in_off, int pos_lo, int pos_hi, Epi&& epi_of, Post&& post,
+                                          const GZ* gz = nullptr) {
   constexpr int R0 = strip_slots<P>();
   if constexpr (P::WLDS) {
     WLds<P, CINP, COUTP> ws{WB};
-    conv_layer<P, CINP, COUTP>(X, R0, in_off, pos_lo, pos_hi, ws, epi_of(ws), post);
+    conv_layer<P, CINP, COUTP, GZIN>(X, R0, in_off, pos_lo, pos_hi, ws, epi_of(ws), post, gz);
   } else {
     WGlb<P, CINP, COUTP> ws{w};
     conv_layer<P, CINP, COUTP>(X, R0, in_off, pos_lo, pos_hi, ws, epi_of(ws), post);
@@ -1355,10 +1400,11 @@ struct FusedNext {
 // [2, R0-2), conv3 over [3, R0-3) with the fused epilogue.  P16: conv1's weights are in
 // WB on entry; each layer's global weight loads for the next layer (conv3: + the
 // aggregation MLP) are issued before its math and stored to WB after it.
-template <class P, int CINP, int CHP, int TAILM>
+template <class P, int CINP, int CHP, int TAILM, bool GZIN = false>
 __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, char* WB, int b, int u,
                                             int f_start, int mode, typename P::Real wm, bool first, int nb = -1,
-                                            int nu = 0, int nfs = 0, FusedNext<P>* fn = nullptr) {
+                                            int nu = 0, int nfs = 0, FusedNext<P>* fn = nullptr,
+                                            const GZ* gz = nullptr) {
   constexpr int R0 = strip_slots<P>();
   const int F = prm.a.F;
   // fused forward: dequeue the item after next here, past the item's prologue waits (an
@@ -1367,14 +1413,14 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
   {
     SepStage<kHID, kHID> nx;
     if constexpr (P::WLDS && kPrefetchW) nx.load(prm.w[1]);
-    run_layer<P, CINP, kHID>(X, WB, prm.w[0], 0, 1, R0 - 1, [&](auto ws) {
-      return EpiInPlace<P, kHID, decltype(ws)>{X, 0, R0 - 1, f_start, F, ws};
+    run_layer<P, CINP, kHID, GZIN>(X, WB, prm.w[0], 0, 1, R0 - 1, [&](auto ws) {
+      return EpiInPlace<P, kHID, decltype(ws), GZIN ? 0 : 2>{X, 0, R0 - 1, f_start, F, ws};
     }, [&]() {
       if constexpr (P::WLDS) {
         if constexpr (!kPrefetchW) nx.load(prm.w[1]);
         nx.store(WB);
       }
-    });
+    }, gz);
   }
   stamp(2);
   {
@@ -1466,8 +1512,8 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
 }
 
 // ---------------------------------------------------------------- per-user block bodies
-// StateInit_m of user u on the strip.  z = [y*ns | pe | h*ns] with each antenna block
-// padded to A2P channels (y at [0, 2A), pe at A2P, A2P+1, h at [A2P+2, A2P+2+2A); the host
+// StateInit_m of user u on the strip.  z = [y*ns | h*ns | pe] with each antenna block
+// padded to A2P channels (y at [0, 2A), h at [A2P, A2P+2A), pe at 2 A2P, 2 A2P + 1; the host
 // packs conv1's weights to match, nrx_api.cpp build_model).  One thread per (slot, symbol)
 // row of the z image: vector loads of the y / h rows and the pe pair, channel assembly in
 // registers at compile-time positions, then 16-byte LDS stores.
@@ -1656,6 +1702,16 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
     }
     float2 pv = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + (ok ? f : 0)) * kT + (ok ? tt : 0)) * 2);
     if (!ok) pv = float2{0.f, 0.f};
+    if constexpr (sizeof(S) == 2) {
+      // one-launch forward: the pe16 chunk of this item's own rows for the update items' conv1
+      // (every slot's StateInit items write the same bytes for a user's rows)
+      if (fn && a.pe16 && ok && lf >= kHalo && lf < kHalo + P::FO) {
+        S pe2[8] = {};
+        pe2[0] = (S)pv.x;
+        pe2[1] = (S)pv.y;
+        *reinterpret_cast<intx4*>(a.pe16 + (((size_t)u * F + f) * kT + tt) * kDS) = *reinterpret_cast<const intx4*>(pe2);
+      }
+    }
     stamp(33);
     if (NRX_INIT_ORDER) {
       if constexpr (P::WLDS) w1.load(prm.w[0]);
@@ -1674,9 +1730,9 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
           const int c = q * P::EPC + e;
           Real v = 0;
           if (c < A2P) v = f32_rounded((Real)yv[c] * ns);
-          else if (c == A2P) v = (Real)pv.x;
-          else if (c == A2P + 1) v = (Real)pv.y;
-          else if (c < 2 * A2P + 2) v = f32_rounded((Real)hv[c - A2P - 2] * ns);
+          else if (c < 2 * A2P) v = f32_rounded((Real)hv[c - A2P] * ns);
+          else if (c == 2 * A2P) v = (Real)pv.x;
+          else if (c == 2 * A2P + 1) v = (Real)pv.y;
           o[e] = (S)v;
         }
         *reinterpret_cast<intx4*>(X + xoff<P, NQZ>(lf, tt, q)) = *reinterpret_cast<const intx4*>(o);
@@ -1689,6 +1745,106 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
   __syncthreads();
   stamp(1);
   strip_block<P, CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 1, wm, first, nb, nu, nfs, fn);
+  stamp(4);
+}
+
+// Zero the pad symbols t = 14, 15 of every slot of the 128-channel strip image (the conv
+// layers never write them; their depthwise reads them as the T = 14 SAME padding).
+template <class P>
+__device__ __forceinline__ void zero_pad_symbols(char* X) {
+  constexpr int NQ = kHID * (int)sizeof(typename P::S) / 16;
+  for (int idx = nrx_tid(); idx < strip_slots<P>() * 2 * NQ; idx += 512) {
+    const int q = idx % NQ, tt = kT + (idx / NQ) % 2, lf = idx / (2 * NQ);
+    *reinterpret_cast<intx4*>(X + xoff<P, NQ>(lf, tt, q)) = intx4{0, 0, 0, 0};
+  }
+}
+
+// One-launch forward StateInit item (f16, 2A = A2P = 8) whose conv1 takes its z rows straight
+// from y / h_hat / pe (GZ): lane (t, g) of K chunk 0 holds channels 8g .. 8g+7 of
+// z = [y*ns | h*ns | pe | 0], i.e. g = 0 the 8 y floats of (f, t), g = 1 the 8 h floats, g = 2
+// the pe pair, g = 3 zeros.  The f32 rows of the wave's conv1 inputs are loaded before the slot
+// norm (their latency behind its reduction), scaled and rounded as the LDS z image is
+// (f32_rounded(v * ns) -> f16), and handed to conv1 as its preloaded chunk: no z image in LDS.
+template <class P, int CHP, int TAILM>
+__device__ __forceinline__ void init_user_gz(const BlockParams<P>& prm, char* smem, int b, int u, int strip,
+                                             typename P::Real wm, bool pads_zero, FusedNext<P>* fn) {
+  __shared__ double red[8];
+  using S = typename P::S;
+  using Real = typename P::Real;
+  constexpr int A2P = 8;
+  constexpr int CINP = init_cinp<A2P>(P::KC);
+  static_assert(CINP == 32 && sizeof(S) == 2, "GZ StateInit: one 32-channel K chunk, f16");
+  constexpr int R0 = strip_slots<P>();
+  const auto& a = prm.a;
+  const int F = a.F, U = a.U;
+  const int f_start = strip * P::FO - kHalo;
+  char* X = smem;
+  char* WB = smem + R0 * slot_pitch<P>();
+  const float* yslot = a.y + (size_t)b * F * kT * A2P;
+  const int nqs = F * kT * A2P / 4;
+  NormPre npre;
+  if (!prm.norm_pre) npre = slot_norm_issue(yslot, nqs);
+  // conv1 rows of this wave (conv_layer's split of the 28 conv1 rows: waves 0-3 four, 4-7 three)
+  const int lane = nrx_tid() & 63, t = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(nrx_tid() >> 6);
+  const int p0 = 1 + 4 * (wave < 4 ? wave : 4) + 3 * (wave > 4 ? wave - 4 : 0);
+  floatx4 raw[6][2];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int f = f_start + p0 - 1 + i;   // wave-uniform
+    const bool row = f >= 0 && f < F && (i < 5 || wave < 4);
+    const int fc = row ? f : 0, tc = t < kT ? t : 0;
+    const size_t re = (size_t)fc * kT + tc;
+    const float* src = (g == 0 || !a.use_h) ? a.y + ((size_t)b * F * kT + re) * A2P
+                     : g == 1 ? a.h_hat + (((size_t)b * U + u) * F * kT + re) * A2P
+                              : a.pe + (((size_t)u * F * kT + re) * 2 & ~(size_t)3);   // 16-B aligned
+    raw[i][0] = *reinterpret_cast<const floatx4*>(src);
+    raw[i][1] = *reinterpret_cast<const floatx4*>(g < 2 ? src + 4 : src);
+  }
+  // the pe16 chunk of this item's own rows for the update items (one (slot, t) row per thread)
+  {
+    const int lf = nrx_tid() / kTP, tt = nrx_tid() % kTP;
+    const int f = f_start + lf;
+    if (a.pe16 && lf >= kHalo && lf < kHalo + P::FO && tt < kT && f >= 0 && f < F) {
+      const float2 pv = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + f) * kT + tt) * 2);
+      S pe2[8] = {};
+      pe2[0] = (S)pv.x;
+      pe2[1] = (S)pv.y;
+      *reinterpret_cast<intx4*>(a.pe16 + (((size_t)u * F + f) * kT + tt) * kDS) = *reinterpret_cast<const intx4*>(pe2);
+    }
+  }
+  SepStage<CINP, kHID> w1;
+  w1.load(prm.w[0]);
+  if (!pads_zero) zero_pad_symbols<P>(X);
+  const Real ns = prm.norm_pre ? (Real)a.norm[b] : (Real)slot_norm(npre, yslot, nqs, red);
+  GZ gz;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int f = f_start + p0 - 1 + i;
+    const bool row = f >= 0 && f < F && t < kT && (g != 1 || a.use_h);
+    S o[8];
+    if (g < 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (S)f32_rounded((Real)(e < 4 ? raw[i][0][e] : raw[i][1][e - 4]) * ns);
+    } else {
+      // the pe pair of (f, t) is the high half of its aligned 16 bytes when its pair index
+      // (u F + f) 14 + t is odd, i.e. when t is odd
+      const bool hi = (t & 1) != 0;
+      const float p0v = hi ? raw[i][0][2] : raw[i][0][0], p1v = hi ? raw[i][0][3] : raw[i][0][1];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (S)0;
+      if (g == 2) {
+        o[0] = (S)p0v;
+        o[1] = (S)p1v;
+      }
+    }
+    half8 h = *reinterpret_cast<const half8*>(o);
+    gz.x0[i] = row ? h : half8{};
+  }
+  w1.store(WB);
+  __syncthreads();
+  stamp(1);
+  strip_block<P, CINP, CHP, TAILM, true>(prm, X, WB, b, u, f_start, 1, wm, true, -1, 0, 0, fn, &gz);
   stamp(4);
 }
 
@@ -1806,6 +1962,64 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
   strip_block<P, kUPD_CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 0, 0, false, nb, nu, nfs, fn);
   stamp(4);
   if (nb >= 0) stamp(32);   // first item of a pair done
+}
+
+#ifndef NRX_INIT_GZ
+#define NRX_INIT_GZ 0    // k_forward StateInit items (2A = 8): conv1 reads y / h_hat / pe directly
+#endif
+#ifndef NRX_FUSED_GZ
+#define NRX_FUSED_GZ 1   // k_forward update items: conv1 reads its z rows from memory (GZ)
+#endif
+
+// A k_forward update item whose conv1 reads the z rows [a | s | pe] straight from memory
+// (GZ): no z image in LDS, hence no z DMA and no pe chunk store; the prologue stages conv1's
+// weights only, and conv1 writes all its output rows before its layer barrier.
+template <class P, int CHP, int TAILM>
+__device__ __forceinline__ void gz_item_run(const BlockParams<P>& prm, char* X, char* WB, int b, int u, int f_start,
+                                            FusedNext<P>* fn, int* psig) {
+  const auto& a = prm.a;
+  SepStage<kUPD_CINP, kHID> w1;
+  w1.load(prm.w[0]);
+  GZ gz;
+  gz.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a.ws_base), 0, (int)a.ws_bytes, 0x00020000);
+  gz.f_start = f_start;
+  gz.F = a.F;
+  const int lane = nrx_tid() & 63, t = lane & 15, g = lane >> 4;
+  auto rel = [&](const void* p) { return (unsigned)(reinterpret_cast<const char*>(p) - a.ws_base); };
+  const unsigned tb = (unsigned)(t * kDS * 2);
+  const unsigned so = rel(a.s_in + srow(b, u, 0, 0, a.U, a.F)) + tb;
+  const unsigned ao = a.U == 2 ? rel(a.a + srow(b, 1 - u, 0, 0, a.U, a.F)) + tb : kGzOob;
+  const unsigned po = rel(a.pe16 + srow(0, u, 0, 0, a.U, a.F)) + tb;
+#pragma unroll
+  for (int kc = 0; kc < 4; ++kc) {
+    const int q = 4 * kc + g;
+    unsigned off = kGzOob;
+    if (t < kT) {
+      if (q < 7) off = ao == kGzOob ? kGzOob : ao + 16u * q;
+      else if (q < 14) off = so + 16u * (q - 7);
+      else if (q == 14) off = po;
+    }
+    gz.off[kc] = off;
+  }
+  // conv1's first K chunk for this wave's rows (conv_layer's split: 28 rows, waves 0-3 four,
+  // 4-7 three), in flight during the weight staging and the barrier
+  {
+    constexpr int R0 = strip_slots<P>();
+    static_assert(R0 - 2 - 24 == 4, "conv1 row split of the 24-row strip: 4 x 4 + 4 x 3");
+    const int wave = __builtin_amdgcn_readfirstlane(nrx_tid() >> 6);
+    const int p0 = 1 + 4 * (wave < 4 ? wave : 4) + 3 * (wave > 4 ? wave - 4 : 0);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) gz.x0[i] = (i < 5 || wave < 4) ? gz.load(0, gz.row_soff(p0 - 1 + i)) : half8{};
+  }
+  // the previous item's stores drain behind these loads; its counter is added once every
+  // wave has drained (deferred signal, k_forward)
+  if (psig) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  w1.store(WB);
+  __syncthreads();
+  if (psig && nrx_tid() == 0) __hip_atomic_fetch_add(psig, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  stamp(1);
+  strip_block<P, kUPD_CINP, CHP, TAILM, true>(prm, X, WB, b, u, f_start, 0, 0, false, -1, 0, 0, fn, &gz);
+  stamp(4);
 }
 
 #ifndef NRX_PAIR
@@ -2159,8 +2373,10 @@ __device__ __forceinline__ void fused_wait(const int* cnt, int need, FusedSync* 
         break;
       }
     }
-    __hip_atomic_fetch_add(&sy->waited, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (it) __hip_atomic_fetch_add(&sy->spins, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (it) {
+      __hip_atomic_fetch_add(&sy->waited, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&sy->spins, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     asm volatile("buffer_inv sc1" ::: "memory");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -2201,6 +2417,9 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
   __syncthreads();
   int j = sh[0], jn = sh[1];
   bool have_z = false;   // item j's z image was DMA'd by the previous item's conv3 hook
+  bool pads_zero = false;   // the strip image's pad symbols were zeroed (by an earlier item)
+  constexpr bool kGz = NRX_FUSED_GZ != 0;
+  int* psig = nullptr;      // GZ: the previous item's dependency counter, not yet added
   auto decode = [&](int jj, int& s, int& b, int& u, int& strip) {
     s = jj / per_stage;
     const int k = jj - s * per_stage;
@@ -2227,33 +2446,64 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
     // the next item's z image is prefetched during this item's conv3 epilogue when its inputs
     // are complete by then (without the prefetch every update item loads its own z image at
     // its start: -4 %, profiles/r03/ab_fused_prefetch.txt)
-    const bool hook = jn < total && sn >= 1;
-    FusedNext<P> fn{&fp.st[hook ? sn : 0], hook ? done + (sn - 1) * B + bn : nullptr, ips, &sh[2], head, 0};
+    // poll: the next item's dependency counter is read (and this CU's L1 invalidated) during
+    // this item's conv2, so that a satisfied next item skips its prologue wait and acquire
+    const bool poll = jn < total && sn >= 1;
+    const bool hook = !kGz && poll;
+    FusedNext<P> fn{&fp.st[poll ? sn : 0], poll ? done + (sn - 1) * B + bn : nullptr, ips, &sh[2], head, 0};
     const int nfs = stn * P::FO - kHalo;
     const int nb = hook ? bn : -1;
+    // deferred signal of the previous item: a GZ update item whose inputs were acquired during
+    // the previous item (no wait) drains and adds it in its prologue, behind its own loads;
+    // otherwise first -- an item that waits must never wait on its own predecessor's signal
+    if (psig && !(kGz && s >= 1 && have_z)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (nrx_tid() == 0) __hip_atomic_fetch_add(psig, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      psig = nullptr;
+    }
     if (s == 0) {
       const auto& a = fp.st[0].a;
       float wm = 1.f;
       if (!a.masking && a.mcs_mask) wm = a.mcs_mask[((size_t)b * U + u) * a.M];
-      init_user<P, A2P, 16, TAIL_AGG>(fp.st[0], smem, b, u, strip, wm, true, nb, un, nfs, &fn);
+      if constexpr (kGz && NRX_INIT_GZ && A2P == 8) {
+        if (a.A == 4) init_user_gz<P, 16, TAIL_AGG>(fp.st[0], smem, b, u, strip, wm, pads_zero, &fn);
+        else init_user<P, A2P, 16, TAIL_AGG>(fp.st[0], smem, b, u, strip, wm, true, nb, un, nfs, &fn);
+      } else {
+        init_user<P, A2P, 16, TAIL_AGG>(fp.st[0], smem, b, u, strip, wm, true, nb, un, nfs, &fn);
+      }
     } else {
       const int fs = strip * P::FO - kHalo;
+      if (kGz && !pads_zero) zero_pad_symbols<P>(X);   // first item of the workgroup
       if (!have_z) fused_wait(done + (s - 1) * B + b, ips, sy, spin_limit);
-      if (s == nst - 1)
+      if (kGz) {
+        if (s == nst - 1) gz_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[s], X, WB, b, u, fs, &fn, psig);
+        else gz_item_run<P, CHP, TAIL_AGG>(fp.st[s], X, WB, b, u, fs, &fn, psig);
+        psig = nullptr;
+      } else if (s == nst - 1)
         dma_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn);
       else
         dma_item_run<P, CHP, TAIL_AGG>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn);
     }
     fstamp(5);
-    // item done: every wave's stores have reached L2, then one add on the slot's counter
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // item done: one add on the slot's counter once every wave's stores have reached L2 --
+    // GZ: deferred to the next item (above / its prologue), so that the store drain overlaps
+    // that item's first loads
+    if (!kGz) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (nrx_tid() == 0) sh[1] = fn.jnn;
     __syncthreads();
-    have_z = hook && sh[2] != 0;
+    have_z = poll && sh[2] != 0;   // GZ: the next item's inputs are complete and acquired
     fstamp(6);
-    if (nrx_tid() == 0) __hip_atomic_fetch_add(done + s * B + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (kGz) psig = done + s * B + b;
+    else if (nrx_tid() == 0) __hip_atomic_fetch_add(done + s * B + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pads_zero = true;
     j = jn;
     jn = sh[1];
+  }
+  if (psig) {   // the last item's deferred signal
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (nrx_tid() == 0) __hip_atomic_fetch_add(psig, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // the last workgroup to leave resets the counters for the next forward
   if (nrx_tid() == 0) {
@@ -2484,7 +2734,7 @@ static bool fused_applicable(const FwdArgs<_Float16, float, _Float16>& a, int nu
   const int cus = cu_count(), nx = xcc_count();
   if (nx < 1 || nx > 8 || cus % nx != 0) return false;
   const long items = (long)a.B * a.U * ((a.F + P::FO - 1) / P::FO);
-  return items >= 2L * cus && a.U <= 2 && a.num_init == 1 && a.H == 1 && 1 + num_it <= kFusedMaxStages &&
+  return items >= 2L * cus && a.ws_bytes < kGzOob && a.pe16 && a.U <= 2 && a.num_init == 1 && a.H == 1 && 1 + num_it <= kFusedMaxStages &&
          2 * a.A <= 16 && a.B <= kFusedMaxB && heads_fit_wb(a.bits_max, 16, 2 * a.A) &&
          strip_slots<P>() * slot_pitch<P>() + kHW2 + 256 * (a.bits_max + 16) <= fused_lds<P>();
 }

@@ -36,7 +36,7 @@ def _generated_case(config, users, prbs, batch, ebno_db, var_mcs, seed):
     torch.cuda.synchronize()
     h = lambda t: t.cpu().numpy()  # noqa: E731
     pe = pe_ref.pe_for_groups(p.num_subcarriers, 14, p.dmrs_symbols, p.cdm_group)
-    mask = h(sb.mcs_mask) if spec.num_mcs > 1 else None
+    mask = h(sb.mcs_mask)   # the oracle takes the one-hot mask for every non-masking model
     case = Case(config, cfg, spec, W.load(cfg.label), h(sb.y), pe, h(sb.h_hat), h(sb.active), mask)
     return case, h(sb.bits), h(sb.mcs), p
 
