@@ -32,18 +32,26 @@ def needs_build() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(d) > t for d in DEPS if os.path.exists(d))
+    if any(os.path.getmtime(d) > t for d in DEPS if os.path.exists(d)):
+        return True
+    return any(_stale(os.path.join(OBJ_DIR, os.path.basename(s) + ".o"), s) for s in SOURCES)
 
 
 HEADERS = [os.path.join(CSRC, "nrx_internal.h"), os.path.join(HERE, "..", "include", "nrx.h")]
 OBJ_DIR = os.path.join(HERE, "lib", "obj")
 
 
+def _sig(src: str) -> str:
+    """mtimes of a source and the headers it includes, taken when its compile starts (an edit
+    made while that compile runs leaves the object stale)"""
+    return " ".join(repr(os.path.getmtime(d)) for d in [src] + HEADERS if os.path.exists(d))
+
+
 def _stale(obj: str, src: str) -> bool:
-    if not os.path.exists(obj):
+    sig = obj + ".sig"
+    if not os.path.exists(obj) or not os.path.exists(sig):
         return True
-    t = os.path.getmtime(obj)
-    return any(os.path.getmtime(d) > t for d in [src] + HEADERS if os.path.exists(d))
+    return open(sig).read() != _sig(src)
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
@@ -65,9 +73,9 @@ def build(force: bool = False, verbose: bool = True) -> str:
         cmd = [hipcc(), *flags, "-c", src, "-o", part]
         if verbose:
             print(" ".join(cmd), flush=True)
-        procs.append((subprocess.Popen(cmd), part, obj))
+        procs.append((subprocess.Popen(cmd), part, obj, _sig(src)))
     bad = 0
-    for p, part, obj in procs:
+    for p, part, obj, sig in procs:
         rc = p.wait()
         if rc:
             bad = rc
@@ -75,6 +83,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
                 os.remove(part)
         else:
             os.replace(part, obj)
+            with open(obj + ".sig", "w") as f:
+                f.write(sig)
     if bad:
         raise subprocess.CalledProcessError(bad, "hipcc -c")
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", *objs, "-o", tmp]

@@ -547,8 +547,7 @@ __device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int
     }
     auto load = [&](int kc) {
       if constexpr (GZIN) {
-        static_assert(sizeof(typename P::S) == 2 && (CINP == 128 || CINP == 32) && R + 2 <= 6,
-                      "global z rows: f16 update conv1 / StateInit conv1 (one preloaded chunk)");
+        static_assert(sizeof(typename P::S) == 2 && CINP == 128 && R + 2 <= 6, "global z rows: f16 update conv1");
         // chunk 0 was issued in the item prologue (its latency behind the conv1-weight staging)
 #pragma unroll
         for (int i = 0; i < R + 2; ++i) xs[i] = kc == 0 ? gz->x0[i] : gz->load(kc, soff[i]);
@@ -1396,6 +1395,7 @@ struct FusedNext {
   int jnn;                      // thread 0: the item dequeued at the start of this block
 };
 
+
 // The three layers of a block, in place: conv1 over positions [1, R0-1), conv2 over
 // [2, R0-2), conv3 over [3, R0-3) with the fused epilogue.  P16: conv1's weights are in
 // WB on entry; each layer's global weight loads for the next layer (conv3: + the
@@ -1759,95 +1759,6 @@ __device__ __forceinline__ void zero_pad_symbols(char* X) {
   }
 }
 
-// One-launch forward StateInit item (f16, 2A = A2P = 8) whose conv1 takes its z rows straight
-// from y / h_hat / pe (GZ): lane (t, g) of K chunk 0 holds channels 8g .. 8g+7 of
-// z = [y*ns | h*ns | pe | 0], i.e. g = 0 the 8 y floats of (f, t), g = 1 the 8 h floats, g = 2
-// the pe pair, g = 3 zeros.  The f32 rows of the wave's conv1 inputs are loaded before the slot
-// norm (their latency behind its reduction), scaled and rounded as the LDS z image is
-// (f32_rounded(v * ns) -> f16), and handed to conv1 as its preloaded chunk: no z image in LDS.
-template <class P, int CHP, int TAILM>
-__device__ __forceinline__ void init_user_gz(const BlockParams<P>& prm, char* smem, int b, int u, int strip,
-                                             typename P::Real wm, bool pads_zero, FusedNext<P>* fn) {
-  __shared__ double red[8];
-  using S = typename P::S;
-  using Real = typename P::Real;
-  constexpr int A2P = 8;
-  constexpr int CINP = init_cinp<A2P>(P::KC);
-  static_assert(CINP == 32 && sizeof(S) == 2, "GZ StateInit: one 32-channel K chunk, f16");
-  constexpr int R0 = strip_slots<P>();
-  const auto& a = prm.a;
-  const int F = a.F, U = a.U;
-  const int f_start = strip * P::FO - kHalo;
-  char* X = smem;
-  char* WB = smem + R0 * slot_pitch<P>();
-  const float* yslot = a.y + (size_t)b * F * kT * A2P;
-  const int nqs = F * kT * A2P / 4;
-  NormPre npre;
-  if (!prm.norm_pre) npre = slot_norm_issue(yslot, nqs);
-  // conv1 rows of this wave (conv_layer's split of the 28 conv1 rows: waves 0-3 four, 4-7 three)
-  const int lane = nrx_tid() & 63, t = lane & 15, g = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(nrx_tid() >> 6);
-  const int p0 = 1 + 4 * (wave < 4 ? wave : 4) + 3 * (wave > 4 ? wave - 4 : 0);
-  floatx4 raw[6][2];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const int f = f_start + p0 - 1 + i;   // wave-uniform
-    const bool row = f >= 0 && f < F && (i < 5 || wave < 4);
-    const int fc = row ? f : 0, tc = t < kT ? t : 0;
-    const size_t re = (size_t)fc * kT + tc;
-    const float* src = (g == 0 || !a.use_h) ? a.y + ((size_t)b * F * kT + re) * A2P
-                     : g == 1 ? a.h_hat + (((size_t)b * U + u) * F * kT + re) * A2P
-                              : a.pe + (((size_t)u * F * kT + re) * 2 & ~(size_t)3);   // 16-B aligned
-    raw[i][0] = *reinterpret_cast<const floatx4*>(src);
-    raw[i][1] = *reinterpret_cast<const floatx4*>(g < 2 ? src + 4 : src);
-  }
-  // the pe16 chunk of this item's own rows for the update items (one (slot, t) row per thread)
-  {
-    const int lf = nrx_tid() / kTP, tt = nrx_tid() % kTP;
-    const int f = f_start + lf;
-    if (a.pe16 && lf >= kHalo && lf < kHalo + P::FO && tt < kT && f >= 0 && f < F) {
-      const float2 pv = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + f) * kT + tt) * 2);
-      S pe2[8] = {};
-      pe2[0] = (S)pv.x;
-      pe2[1] = (S)pv.y;
-      *reinterpret_cast<intx4*>(a.pe16 + (((size_t)u * F + f) * kT + tt) * kDS) = *reinterpret_cast<const intx4*>(pe2);
-    }
-  }
-  SepStage<CINP, kHID> w1;
-  w1.load(prm.w[0]);
-  if (!pads_zero) zero_pad_symbols<P>(X);
-  const Real ns = prm.norm_pre ? (Real)a.norm[b] : (Real)slot_norm(npre, yslot, nqs, red);
-  GZ gz;
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const int f = f_start + p0 - 1 + i;
-    const bool row = f >= 0 && f < F && t < kT && (g != 1 || a.use_h);
-    S o[8];
-    if (g < 2) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (S)f32_rounded((Real)(e < 4 ? raw[i][0][e] : raw[i][1][e - 4]) * ns);
-    } else {
-      // the pe pair of (f, t) is the high half of its aligned 16 bytes when its pair index
-      // (u F + f) 14 + t is odd, i.e. when t is odd
-      const bool hi = (t & 1) != 0;
-      const float p0v = hi ? raw[i][0][2] : raw[i][0][0], p1v = hi ? raw[i][0][3] : raw[i][0][1];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (S)0;
-      if (g == 2) {
-        o[0] = (S)p0v;
-        o[1] = (S)p1v;
-      }
-    }
-    half8 h = *reinterpret_cast<const half8*>(o);
-    gz.x0[i] = row ? h : half8{};
-  }
-  w1.store(WB);
-  __syncthreads();
-  stamp(1);
-  strip_block<P, CINP, CHP, TAILM, true>(prm, X, WB, b, u, f_start, 1, wm, true, -1, 0, 0, fn, &gz);
-  stamp(4);
-}
-
 // Waves that issue the paired next item's z DMA: 0-3.  A burst of LDS-DMA issues stalls the
 // issuing wave; with four issuing waves one wave of each SIMD pair issues while the other runs
 // its epilogue (all eight: -1.5 %, after the item: -2.1 %, split before / after the epilogue:
@@ -1964,9 +1875,6 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
   if (nb >= 0) stamp(32);   // first item of a pair done
 }
 
-#ifndef NRX_INIT_GZ
-#define NRX_INIT_GZ 0    // k_forward StateInit items (2A = 8): conv1 reads y / h_hat / pe directly
-#endif
 #ifndef NRX_FUSED_GZ
 #define NRX_FUSED_GZ 1   // k_forward update items: conv1 reads its z rows from memory (GZ)
 #endif
@@ -2450,8 +2358,8 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
     // this item's conv2, so that a satisfied next item skips its prologue wait and acquire
     const bool poll = jn < total && sn >= 1;
     const bool hook = !kGz && poll;
-    FusedNext<P> fn{&fp.st[poll ? sn : 0], poll ? done + (sn - 1) * B + bn : nullptr, ips, &sh[2], head, 0};
     const int nfs = stn * P::FO - kHalo;
+    FusedNext<P> fn{&fp.st[poll ? sn : 0], poll ? done + (sn - 1) * B + bn : nullptr, ips, &sh[2], head, 0};
     const int nb = hook ? bn : -1;
     // deferred signal of the previous item: a GZ update item whose inputs were acquired during
     // the previous item (no wait) drains and adds it in its prologue, behind its own loads;
@@ -2466,12 +2374,7 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
       const auto& a = fp.st[0].a;
       float wm = 1.f;
       if (!a.masking && a.mcs_mask) wm = a.mcs_mask[((size_t)b * U + u) * a.M];
-      if constexpr (kGz && NRX_INIT_GZ && A2P == 8) {
-        if (a.A == 4) init_user_gz<P, 16, TAIL_AGG>(fp.st[0], smem, b, u, strip, wm, pads_zero, &fn);
-        else init_user<P, A2P, 16, TAIL_AGG>(fp.st[0], smem, b, u, strip, wm, true, nb, un, nfs, &fn);
-      } else {
-        init_user<P, A2P, 16, TAIL_AGG>(fp.st[0], smem, b, u, strip, wm, true, nb, un, nfs, &fn);
-      }
+      init_user<P, A2P, 16, TAIL_AGG>(fp.st[0], smem, b, u, strip, wm, true, nb, un, nfs, &fn);
     } else {
       const int fs = strip * P::FO - kHalo;
       if (kGz && !pads_zero) zero_pad_symbols<P>(X);   // first item of the workgroup

@@ -2,6 +2,7 @@
 # library and named variant libraries (neural_rx_amd/lib/var/<name>/libnrx.so).
 # usage (GPU box): bash tools/gpu_r04_ab.sh <tag> <rounds> [notests] <var>...
 set -o pipefail
+set -e
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/$1; R=$2; shift 2
 mkdir -p $O
