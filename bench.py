@@ -334,12 +334,14 @@ def main():
         if fused_st["error"]:
             print(f"bench.py: one-launch forward error bits {fused_st['error']}: outputs invalid", file=sys.stderr)
 
+    _progress(f"timed region done: {value:.0f} slots/s")
     # ---- batch-1 per-slot latency (hipGraph replay; device-only and H2D+compute+D2H)
     latency = None
     if not args.no_latency and rank == 0:
         latency = measure_latency(torch, eng, spec, cfg, args, groups, dev, num_it)
         latency["132prb_aerial_contract"] = measure_latency_aerial(torch, eng, spec, cfg, args, groups, dev, num_it)
 
+    _progress("latency done")
     # ---- end-to-end Monte-Carlo step on the GPU: generate + receive + count (not `value`)
     e2e = None
     if not args.no_e2e:
@@ -537,6 +539,32 @@ def measure_latency_aerial(torch, eng, spec, cfg, args, groups, dev, num_it, prb
             "batch1_slots_per_s_e2e": round(1e3 / float(np.median(e2e)), 1)}
 
 
+def _progress(msg):
+    """one stderr line per bench phase (a long silent phase looks hung to a supervisor)"""
+    print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_quota():
+    """CPUs this process may use: the affinity set, capped by a cgroup CPU quota when one is set
+    (a box may expose every host CPU to the affinity mask while its cgroup grants a share of them;
+    one torch thread per exposed CPU then oversubscribes the share many times over)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    return (min(n, quota) if quota else n), n, quota
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -562,10 +590,10 @@ def cpu_baseline(spec, cfg, slots, pe_np, args, num_it):
     from neural_rx_amd.config import dmrs_symbols, user_cdm_groups
     from neural_rx_amd.receiver import compute_pe
     model = TorchCGNN(cgnn_ref.split_keras_weights(W.load(cfg.label), spec), spec)
-    # torch.set_num_threads(os.cpu_count()) -- the CPUs this process may run on
-    # (the affinity set; os.cpu_count() where the platform has none)
+    # torch.set_num_threads(os.cpu_count()) -- here the CPUs this process may run on:
+    # the affinity set, capped by the cgroup CPU quota (cpu_quota)
     torch_default = torch.get_num_threads()
-    all_threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    all_threads, affinity, quota = cpu_quota()
     B, U = slots.y.shape[0], slots.h_hat.shape[1]
     ones = lambda b, u: np.ones((b, u, spec.num_mcs), np.float32)
     # cfg 1: one user, batch 1 (same trained weights, 4 PRB)
@@ -589,18 +617,19 @@ def cpu_baseline(spec, cfg, slots, pe_np, args, num_it):
 
     res = {}
     for tag, th in (("all", all_threads), ("1thread", 1)):
+        _progress(f"cpu baseline, {th} threads")
         torch.set_num_threads(th)
         res[tag] = {"threads": th, "cfg1_b1_p50_ms": round(p50_b1(40 if th > 1 else 25), 3),
                     "cfg2_b128_slots_per_s": round(b128(2 if th > 1 else 1), 2)}
     torch.set_num_threads(torch_default)
     return {"value": res["all"]["cfg2_b128_slots_per_s"], "unit": "slots/s", "cores": all_threads,
-            "threads": all_threads, "torch_default_threads": torch_default,
+            "threads": all_threads, "torch_default_threads": torch_default, "cgroup_cpu_quota": quota,
             "kind": "port",
             "sample": f"torch-CPU fp32 restatement (oracle/cgnn_torch.py), bench workload cfg2 "
                       f"({B} slots, {U} users, {args.prbs} PRB, num_it {num_it}) x2 batches at {all_threads} threads "
                       f"(value), plus cfg1 (1 UE, B=1) p50 latency and 1-thread runs",
             "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(),
-            "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+            "affinity_cpus": affinity,
             "all_threads": res["all"], "one_thread": res["1thread"]}
 
 

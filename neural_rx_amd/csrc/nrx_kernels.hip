@@ -1875,9 +1875,6 @@ __device__ __forceinline__ void dma_item_run(const BlockParams<P>& prm, char* X,
   if (nb >= 0) stamp(32);   // first item of a pair done
 }
 
-#ifndef NRX_FUSED_GZ
-#define NRX_FUSED_GZ 1   // k_forward update items: conv1 reads its z rows from memory (GZ)
-#endif
 
 // A k_forward update item whose conv1 reads the z rows [a | s | pe] straight from memory
 // (GZ): no z image in LDS, hence no z DMA and no pe chunk store; the prologue stages conv1's
@@ -2242,7 +2239,9 @@ struct FusedSync {
   int pad[4];
   // int done[kFusedMaxStages][B] follows
 };
-constexpr int kFusedMaxStages = 4;   // StateInit + up to 3 updates
+constexpr int kFusedMaxStages = 12;  // StateInit (x M for Var-IO) + the updates (8 for nrx_large);
+                                     // FusedParams ~7.5 KB of kernel arguments (16 KB measured to
+                                     // pass, tools/ubench/kernarg.hip)
 // dynamic LDS of k_forward: the paired-readout layout minus room for the static __shared__
 // words (the slot-norm reduction of StateInit, the queue words); the readout heads must fit
 constexpr int kFusedLds = 160 * 1024 - 256;
@@ -2257,9 +2256,11 @@ constexpr size_t kFusedSyncBytes = sizeof(FusedSync) + (size_t)kFusedMaxStages *
 
 template <class P>
 struct FusedParams {
-  BlockParams<P> st[kFusedMaxStages];   // 0: StateInit (aggregation tail), 1..nst-1: updates
+  BlockParams<P> st[kFusedMaxStages];   // 0..ninit-1: StateInit m, ninit..nst-1: updates
   FusedSync* sync;
-  int nst;                              // 1 + num_it
+  int nst;                              // ninit + num_it
+  int ninit;                            // StateInit stages (M for Var-IO, else 1)
+  int heads_x;                          // readout heads staged in the strip image (H > 1)
   int nq;                               // queues (XCDs)
   int spin_limit;                       // dependency-wait polls before the timeout error
   int dbg_err;                          // debug: error bits workgroup 0 sets (nrx_debug_fused)
@@ -2304,7 +2305,7 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
   char* WB = smem + R0 * slot_pitch<P>();
   FusedSync* sy = fp_arg.sync;   // scalars straight from the parameter (keeps it in the kernarg list)
   int* done = reinterpret_cast<int*>(sy + 1);
-  const int nst = fp_arg.nst, nqs = fp_arg.nq, spin_limit = fp_arg.spin_limit;
+  const int nst = fp_arg.nst, ninit = fp_arg.ninit, nqs = fp_arg.nq, spin_limit = fp_arg.spin_limit;
   const auto& a0 = fp.st[0].a;
   const int B = a0.B, U = a0.U, strips = fp.st[0].strips;
   const int ips = U * strips;   // items per (stage, slot) = a slot's dependency count
@@ -2324,10 +2325,9 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
   }
   __syncthreads();
   int j = sh[0], jn = sh[1];
-  bool have_z = false;   // item j's z image was DMA'd by the previous item's conv3 hook
+  bool have_z = false;      // item j's inputs were complete and acquired during the previous item
   bool pads_zero = false;   // the strip image's pad symbols were zeroed (by an earlier item)
-  constexpr bool kGz = NRX_FUSED_GZ != 0;
-  int* psig = nullptr;      // GZ: the previous item's dependency counter, not yet added
+  int* psig = nullptr;      // the previous item's dependency counter, not yet added
   auto decode = [&](int jj, int& s, int& b, int& u, int& strip) {
     s = jj / per_stage;
     const int k = jj - s * per_stage;
@@ -2351,55 +2351,48 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
 #endif
     int sn = 0, bn = 0, un = 0, stn = 0;
     if (jn < total) decode(jn, sn, bn, un, stn);
-    // the next item's z image is prefetched during this item's conv3 epilogue when its inputs
-    // are complete by then (without the prefetch every update item loads its own z image at
-    // its start: -4 %, profiles/r03/ab_fused_prefetch.txt)
     // poll: the next item's dependency counter is read (and this CU's L1 invalidated) during
     // this item's conv2, so that a satisfied next item skips its prologue wait and acquire
     const bool poll = jn < total && sn >= 1;
-    const bool hook = !kGz && poll;
-    const int nfs = stn * P::FO - kHalo;
     FusedNext<P> fn{&fp.st[poll ? sn : 0], poll ? done + (sn - 1) * B + bn : nullptr, ips, &sh[2], head, 0};
-    const int nb = hook ? bn : -1;
-    // deferred signal of the previous item: a GZ update item whose inputs were acquired during
+    // deferred signal of the previous item: an update item whose inputs were acquired during
     // the previous item (no wait) drains and adds it in its prologue, behind its own loads;
     // otherwise first -- an item that waits must never wait on its own predecessor's signal
-    if (psig && !(kGz && s >= 1 && have_z)) {
+    if (psig && !(s >= ninit && have_z)) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (nrx_tid() == 0) __hip_atomic_fetch_add(psig, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       psig = nullptr;
     }
-    if (s == 0) {
-      const auto& a = fp.st[0].a;
+    if (s >= 1 && !have_z) fused_wait(done + (s - 1) * B + b, ips, sy, spin_limit);
+    if (s < ninit) {
+      // StateInit m = s (Var-IO: one stage per MCS, accumulating s = sum_m mask_m SI_m,
+      // neural_rx.py:562-569; the last one applies iteration 0's aggregation MLP)
+      const auto& a = fp.st[s].a;
       float wm = 1.f;
-      if (!a.masking && a.mcs_mask) wm = a.mcs_mask[((size_t)b * U + u) * a.M];
-      init_user<P, A2P, 16, TAIL_AGG>(fp.st[0], smem, b, u, strip, wm, true, nb, un, nfs, &fn);
+      if (!a.masking) wm = a.mcs_mask ? a.mcs_mask[((size_t)b * U + u) * a.M + s] : (s == 0 ? 1.f : 0.f);
+      if (s == ninit - 1) init_user<P, A2P, 16, TAIL_AGG>(fp.st[s], smem, b, u, strip, wm, s == 0, -1, 0, 0, &fn);
+      else init_user<P, A2P, 16, TAIL_NONE>(fp.st[s], smem, b, u, strip, wm, s == 0, -1, 0, 0, &fn);
     } else {
       const int fs = strip * P::FO - kHalo;
-      if (kGz && !pads_zero) zero_pad_symbols<P>(X);   // first item of the workgroup
-      if (!have_z) fused_wait(done + (s - 1) * B + b, ips, sy, spin_limit);
-      if (kGz) {
-        if (s == nst - 1) gz_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[s], X, WB, b, u, fs, &fn, psig);
-        else gz_item_run<P, CHP, TAIL_AGG>(fp.st[s], X, WB, b, u, fs, &fn, psig);
-        psig = nullptr;
-      } else if (s == nst - 1)
-        dma_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn);
-      else
-        dma_item_run<P, CHP, TAIL_AGG>(fp.st[s], X, WB, b, u, fs, nb, un, nfs, !have_z, &fn);
+      if (!pads_zero) zero_pad_symbols<P>(X);   // first item of the workgroup
+      if (s < nst - 1) gz_item_run<P, CHP, TAIL_AGG>(fp.st[s], X, WB, b, u, fs, &fn, psig);
+      else if (fp_arg.heads_x) gz_item_run<P, CHP, TAIL_READOUT>(fp.st[s], X, WB, b, u, fs, &fn, psig);
+      else gz_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[s], X, WB, b, u, fs, &fn, psig);
+      psig = nullptr;
     }
     fstamp(5);
     // item done: one add on the slot's counter once every wave's stores have reached L2 --
-    // GZ: deferred to the next item (above / its prologue), so that the store drain overlaps
-    // that item's first loads
-    if (!kGz) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // deferred to the next item (above / its prologue), so that the store drain overlaps that
+    // item's first loads
     if (nrx_tid() == 0) sh[1] = fn.jnn;
     __syncthreads();
-    have_z = poll && sh[2] != 0;   // GZ: the next item's inputs are complete and acquired
+    have_z = poll && sh[2] != 0;   // the next item's inputs are complete and acquired
     fstamp(6);
-    if (kGz) psig = done + s * B + b;
-    else if (nrx_tid() == 0) __hip_atomic_fetch_add(done + s * B + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    pads_zero = true;
+    psig = done + s * B + b;
+    // a readout item with its heads in the strip image (TAIL_READOUT, H > 1) overwrote the pad
+    // symbols: the next item zeroes them again
+    pads_zero = !(s == nst - 1 && fp_arg.heads_x);
     j = jn;
     jn = sh[1];
   }
@@ -2637,9 +2630,13 @@ static bool fused_applicable(const FwdArgs<_Float16, float, _Float16>& a, int nu
   const int cus = cu_count(), nx = xcc_count();
   if (nx < 1 || nx > 8 || cus % nx != 0) return false;
   const long items = (long)a.B * a.U * ((a.F + P::FO - 1) / P::FO);
-  return items >= 2L * cus && a.ws_bytes < kGzOob && a.pe16 && a.U <= 2 && a.num_init == 1 && a.H == 1 && 1 + num_it <= kFusedMaxStages &&
-         2 * a.A <= 16 && a.B <= kFusedMaxB && heads_fit_wb(a.bits_max, 16, 2 * a.A) &&
-         strip_slots<P>() * slot_pitch<P>() + kHW2 + 256 * (a.bits_max + 16) <= fused_lds<P>();
+  // readout heads: one LLR head in WB (TAIL_READOUT_WB), or up to three + ChEst in the strip
+  // image (TAIL_READOUT, X layout)
+  const bool heads = a.H == 1 ? heads_fit_wb(a.bits_max, 16, 2 * a.A) &&
+                                    strip_slots<P>() * slot_pitch<P>() + kHW2 + 256 * (a.bits_max + 16) <= fused_lds<P>()
+                              : a.H <= 3 && (a.H + 1) * (kHeadSlot + 1024) <= strip_slots<P>() * slot_pitch<P>();
+  return items >= 2L * cus && a.ws_bytes < kGzOob && a.pe16 && a.U <= 2 && a.num_init + num_it <= kFusedMaxStages &&
+         2 * a.A <= 16 && a.B <= kFusedMaxB && a.bits_max <= 16 && heads;
 }
 
 template <class P>
@@ -2647,7 +2644,9 @@ static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, cons
                             int num_it, hipStream_t st, Prof* prof, const FusedCtl& fc) {
   FusedParams<P> fp{};
   fp.sync = reinterpret_cast<FusedSync*>(fc.sync);
-  fp.nst = 1 + num_it;
+  fp.ninit = args.num_init;
+  fp.nst = args.num_init + num_it;
+  fp.heads_x = args.H > 1;
   const int cus = cu_count();
   fp.nq = xcc_count();
   fp.spin_limit = fc.spin_limit;
@@ -2676,18 +2675,21 @@ static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, cons
     }
     bp.chest[0] = W.chest[0];
     bp.chest[1] = W.chest[1];
-    if (s == 0) {
-      for (int l = 0; l < 3; ++l) bp.w[l] = W.init[0][l];
-      bp.tail = TAIL_AGG;
+    if (s < fp.ninit) {
+      // StateInit m = s into s_out (m > 0 accumulating); the last one runs iteration 0's
+      // aggregation MLP
+      for (int l = 0; l < 3; ++l) bp.w[l] = W.init[s][l];
+      bp.m = s;
+      bp.tail = s == fp.ninit - 1 ? TAIL_AGG : TAIL_NONE;
       bp.agg[0] = W.agg[0][0];
       bp.agg[1] = W.agg[0][1];
     } else {
       std::swap(a.s_in, a.s_out);
       std::swap(a.a, a.a_out);
-      const int i = s - 1;
+      const int i = s - fp.ninit;
       for (int l = 0; l < 3; ++l) bp.w[l] = W.upd[i][l];
       const bool last = i == num_it - 1;
-      bp.tail = last ? TAIL_READOUT_WB : TAIL_AGG;
+      bp.tail = last ? (fp.heads_x ? TAIL_READOUT : TAIL_READOUT_WB) : TAIL_AGG;
       if (!last) {
         bp.agg[0] = W.agg[i + 1][0];
         bp.agg[1] = W.agg[i + 1][1];

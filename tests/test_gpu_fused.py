@@ -69,6 +69,22 @@ def test_fused_num_it_1_identical():
     _check_identical(case)
 
 
+def test_fused_var_io_identical():
+    # BASELINE cfg4 per-GPU shard: Var-IO (two accumulating StateInit stages, two LLR heads
+    # staged in the strip image at the readout), random MCS per (slot, user)
+    rng = np.random.default_rng(39)
+    mcs = rng.integers(0, 2, size=(128, 2))
+    _check_identical(make_case("nrx_rt_var_mcs", batch=128, users=2, prbs=4, snr_db=12, seed=39, mcs_choice=mcs))
+
+
+def test_fused_8_iterations_identical():
+    # BASELINE cfg4' per-GPU shard: the masking model, 8 iterations (nine stages), 6-bit head
+    rng = np.random.default_rng(40)
+    mcs = rng.integers(0, 3, size=(128, 2))
+    _check_identical(make_case("nrx_large_var_mcs_64qam_masking", batch=128, users=2, prbs=4, snr_db=22, seed=40,
+                               mcs_choice=mcs))
+
+
 def test_fused_odd_batch_identical():
     # B not a multiple of the 8 queues: queues hold 17 or 16 slots
     _check_identical(make_case("nrx_rt", batch=131, users=2, prbs=4, snr_db=12, seed=35))
