@@ -1893,7 +1893,11 @@ __device__ __forceinline__ void gz_item_run(const BlockParams<P>& prm, char* X, 
   auto rel = [&](const void* p) { return (unsigned)(reinterpret_cast<const char*>(p) - a.ws_base); };
   const unsigned tb = (unsigned)(t * kDS * 2);
   const unsigned so = rel(a.s_in + srow(b, u, 0, 0, a.U, a.F)) + tb;
-  const unsigned ao = a.U == 2 ? rel(a.a + srow(b, 1 - u, 0, 0, a.U, a.F)) + tb : kGzOob;
+  // a: the other user's act*sp plane (U = 2, p = 1), none (U = 1), or the combined a_u plane
+  // (U > 4: a combine stage ran in place)
+  const unsigned ao = !prm.inline_combine ? rel(a.a + srow(b, u, 0, 0, a.U, a.F)) + tb
+                      : a.U == 2          ? rel(a.a + srow(b, 1 - u, 0, 0, a.U, a.F)) + tb
+                                          : kGzOob;
   const unsigned po = rel(a.pe16 + srow(0, u, 0, 0, a.U, a.F)) + tb;
 #pragma unroll
   for (int kc = 0; kc < 4; ++kc) {
@@ -1953,8 +1957,12 @@ __device__ __forceinline__ void update_pair(const BlockParams<P>& prm, char* sme
 }
 
 // UpdateState of user u on the strip (z = [a, s, pe]).
+// fn / psig: a k_forward item (U > 2: the z image with the inline leave-one-out combine is
+// staged here, not read by conv1 from memory): the next item's dependency poll, and the
+// previous item's deferred counter add (after this item's loads and the layer barrier).
 template <class P, int CHP, int TAILM>
-__device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* smem, int b, int u, int strip) {
+__device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* smem, int b, int u, int strip,
+                                            FusedNext<P>* fn = nullptr, int* psig = nullptr) {
   using S = typename P::S;
   constexpr int R0 = strip_slots<P>();
   constexpr int NQ = kUPD_CINP * (int)sizeof(S) / 16;  // chunks per z row
@@ -1966,7 +1974,7 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
   char* X = smem;
   char* WB = smem + R0 * slot_pitch<P>();
   if constexpr (sizeof(S) == 2 && NRX_ZDMA != 0) {
-    if (prm.inline_combine && U <= 2) {
+    if (prm.inline_combine && U <= 2 && !fn) {
       if (!NRX_W1_FIRST) zload_dma_u2<P>(prm, X, b, u, f_start);
       dma_item_run<P, CHP, TAILM>(prm, X, WB, b, u, f_start, -1, 0, 0, NRX_W1_FIRST != 0);
       return;
@@ -2089,9 +2097,11 @@ __device__ __forceinline__ void update_user(const BlockParams<P>& prm, char* sme
   stamp(26);
   if constexpr (P::WLDS) w1.store(WB);
   stamp(27);
+  if (psig) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the previous item's stores
   __syncthreads();
+  if (psig && nrx_tid() == 0) __hip_atomic_fetch_add(psig, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp(1);
-  strip_block<P, kUPD_CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 0, 0, false);
+  strip_block<P, kUPD_CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 0, 0, false, -1, 0, 0, fn);
   stamp(4);
 }
 
@@ -2155,7 +2165,7 @@ __global__ __launch_bounds__(256) void k_combine(typename P::S* __restrict__ buf
     const S* sv = reinterpret_cast<const S*>(&v);
     S o[P::EPC];
 #pragma unroll
-    for (int e = 0; e < P::EPC; ++e) o[e] = (S)((sum[e] - (Real)sv[e]) * p);
+    for (int e = 0; e < P::EPC; ++e) o[e] = (S)f32_rounded((sum[e] - (Real)sv[e]) * p);
     *reinterpret_cast<intx4*>(base + u * ustride) = *reinterpret_cast<const intx4*>(o);
   }
 }
@@ -2252,7 +2262,10 @@ constexpr int fused_lds() {
   return strip_lds_bytes<P>(true) > kFusedLds ? kFusedLds : strip_lds_bytes<P>(true);
 }
 constexpr int kFusedMaxB = 65536;
-constexpr size_t kFusedSyncBytes = sizeof(FusedSync) + (size_t)kFusedMaxStages * kFusedMaxB * sizeof(int);
+// logical stages: the StateInit stages, then per iteration (U > kInlineUsers) a combine stage
+// and the update stage; one dependency counter row each
+constexpr int kFusedMaxLS = 20;
+constexpr size_t kFusedSyncBytes = sizeof(FusedSync) + (size_t)kFusedMaxLS * kFusedMaxB * sizeof(int);
 
 template <class P>
 struct FusedParams {
@@ -2260,7 +2273,13 @@ struct FusedParams {
   FusedSync* sync;
   int nst;                              // ninit + num_it
   int ninit;                            // StateInit stages (M for Var-IO, else 1)
+  int nls;                              // logical stages (GEN)
+  int kind[kFusedMaxLS];                // GEN: 0 StateInit, 1 update, 2 leave-one-out combine
+  int pidx[kFusedMaxLS];                // GEN: the stage's st[] entry (combine: its update's)
   int heads_x;                          // readout heads staged in the strip image (H > 1)
+  int gz;                               // update items: conv1 reads z from memory (U <= 2, the
+                                        // workspace within the 32-bit buffer range); else
+                                        // the z image is staged in LDS (update_user)
   int nq;                               // queues (XCDs)
   int spin_limit;                       // dependency-wait polls before the timeout error
   int dbg_err;                          // debug: error bits workgroup 0 sets (nrx_debug_fused)
@@ -2292,6 +2311,60 @@ __device__ __forceinline__ void fused_wait(const int* cnt, int need, FusedSync* 
   __syncthreads();
 }
 
+// A combine item of k_forward (U > kInlineUsers): the leave-one-out mean of one (slot, strip),
+// in place over the act*sp rows of every user -- k_combine's arithmetic (f32 sum over u in
+// order, then (sum - sp_u) * p), so the outputs equal the three-launch forward's.  Its rows
+// are its own strip's (no halo); the next update stage waits for all strips of the slot.  It
+// runs no conv2, so the next item's dependency poll is done at its end.
+template <class P>
+__device__ __forceinline__ void combine_item(const BlockParams<P>& prm, int b, int strip, FusedNext<P>* fn) {
+  using S = typename P::S;
+  using Real = typename P::Real;
+  constexpr int QS = kDS / P::EPC;
+  if (nrx_tid() == 0) fn->jnn = atomicAdd(fn->head, 1);
+  const auto& a = prm.a;
+  const int U = a.U, F = a.F;
+  const int f0 = strip * P::FO, f1 = f0 + P::FO < F ? f0 + P::FO : F;
+  const size_t ustride = (size_t)F * kT * kDS;
+  S* buf = const_cast<S*>(a.a) + (size_t)b * U * ustride + (size_t)f0 * kT * kDS;
+  Real nact = 0;
+  for (int uu = 0; uu < U; ++uu) nact += (Real)a.active[(size_t)b * U + uu];
+  Real p = nact - (Real)1;
+  p = p > (Real)0 ? (Real)1 / p : (Real)1;
+  const int n = (f1 - f0) * kT * QS;
+  for (int idx = nrx_tid(); idx < n; idx += 512) {
+    S* base = buf + (size_t)(idx / QS) * kDS + (idx % QS) * P::EPC;
+    Real sum[P::EPC];
+#pragma unroll
+    for (int e = 0; e < P::EPC; ++e) sum[e] = 0;
+    for (int uu = 0; uu < U; ++uu) {
+      const intx4 v = *reinterpret_cast<const intx4*>(base + uu * ustride);
+      const S* sv = reinterpret_cast<const S*>(&v);
+#pragma unroll
+      for (int e = 0; e < P::EPC; ++e) sum[e] += (Real)sv[e];
+    }
+    for (int uu = 0; uu < U; ++uu) {
+      const intx4 v = *reinterpret_cast<const intx4*>(base + uu * ustride);
+      const S* sv = reinterpret_cast<const S*>(&v);
+      S o[P::EPC];
+#pragma unroll
+      // rounded to f32 before the storage conversion (as k_combine: no fused single-rounding
+      // multiply-convert in one kernel family and not in the other)
+      for (int e = 0; e < P::EPC; ++e) o[e] = (S)f32_rounded((sum[e] - (Real)sv[e]) * p);
+      *reinterpret_cast<intx4*>(base + uu * ustride) = *reinterpret_cast<const intx4*>(o);
+    }
+  }
+  if (nrx_tid() == 0) {
+    int v = 0;
+    if (fn->ndone) {
+      v = __hip_atomic_load(fn->ndone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= fn->nneed;
+      asm volatile("buffer_inv sc1" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *fn->nflag = v;
+  }
+}
+
 // GEN: the general stage list (Var-IO StateInit stages, readout heads in the strip image);
 // the plain kernel keeps only the one-StateInit / one-head code (its code size -- 141 KB
 // against 237 KB -- measured 3.5 % faster, profiles/r04/ab_fused_gen.txt)
@@ -2314,7 +2387,27 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
   const int ips = U * strips;   // items per (stage, slot) = a slot's dependency count
   const int q = xcc_id() % nqs;
   const int nbq = (B - q + nqs - 1) / nqs;
-  const int per_stage = nbq * ips, total = nst * per_stage;
+  const int per_stage = nbq * ips;
+  // logical stages: the plain kernel has StateInit stages then updates, ips items per slot
+  // each; GEN adds a combine stage (one item per (slot, strip)) before each update when U > 4
+  const int nls = GEN ? fp_arg.nls : nst;
+  auto kind_of = [&](int ls) -> int {
+    if constexpr (GEN) return fp.kind[ls];
+    else return ls < ninit ? 0 : 1;
+  };
+  auto pidx_of = [&](int ls) -> int {
+    if constexpr (GEN) return fp.pidx[ls];
+    else return ls;
+  };
+  auto ips_of = [&](int ls) -> int {
+    if constexpr (GEN) return fp.kind[ls] == 2 ? strips : ips;
+    else return ips;
+  };
+  int total = nst * per_stage;
+  if constexpr (GEN) {
+    total = 0;
+    for (int ls = 0; ls < nls; ++ls) total += nbq * ips_of(ls);
+  }
   int* head = &sy->head[q];
   if (nrx_tid() == 0) {
     // two separate dequeues: with one atomic for both (round 3, d1f0f90) a workgroup's first
@@ -2332,11 +2425,23 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
   bool pads_zero = false;   // the strip image's pad symbols were zeroed (by an earlier item)
   int* psig = nullptr;      // the previous item's dependency counter, not yet added
   auto decode = [&](int jj, int& s, int& b, int& u, int& strip) {
-    s = jj / per_stage;
-    const int k = jj - s * per_stage;
-    b = q + nqs * (k / ips);
-    u = (k % ips) / strips;
-    strip = k % strips;
+    int k = jj, ip = ips;
+    if constexpr (GEN) {
+      s = 0;
+      for (;;) {
+        ip = ips_of(s);
+        if (k < nbq * ip || s == nls - 1) break;
+        k -= nbq * ip;
+        ++s;
+      }
+    } else {
+      s = jj / per_stage;
+      k = jj - s * per_stage;
+    }
+    b = q + nqs * (k / ip);
+    const int r = k % ip;
+    u = GEN && kind_of(s) == 2 ? 0 : r / strips;
+    strip = r % strips;
   };
 #ifdef NRX_STAMPS
   int n_item = 0;
@@ -2357,18 +2462,20 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
     // poll: the next item's dependency counter is read (and this CU's L1 invalidated) during
     // this item's conv2, so that a satisfied next item skips its prologue wait and acquire
     const bool poll = jn < total && sn >= 1;
-    FusedNext<P> fn{&fp.st[poll ? sn : 0], poll ? done + (sn - 1) * B + bn : nullptr, ips, &sh[2], head, 0};
+    FusedNext<P> fn{&fp.st[poll ? pidx_of(sn) : 0], poll ? done + (sn - 1) * B + bn : nullptr,
+                    poll ? ips_of(sn - 1) : ips, &sh[2], head, 0};
+    const int kd = kind_of(s), ps = pidx_of(s);
     // deferred signal of the previous item: an update item whose inputs were acquired during
     // the previous item (no wait) drains and adds it in its prologue, behind its own loads;
     // otherwise first -- an item that waits must never wait on its own predecessor's signal
-    if (psig && !(s >= ninit && have_z)) {
+    if (psig && !(kd == 1 && have_z)) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (nrx_tid() == 0) __hip_atomic_fetch_add(psig, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       psig = nullptr;
     }
-    if (s >= 1 && !have_z) fused_wait(done + (s - 1) * B + b, ips, sy, spin_limit);
-    if (s < ninit) {
+    if (s >= 1 && !have_z) fused_wait(done + (s - 1) * B + b, ips_of(s - 1), sy, spin_limit);
+    if (kd == 0) {
       // StateInit m = s (Var-IO: one stage per MCS, accumulating s = sum_m mask_m SI_m,
       // neural_rx.py:562-569; the last one applies iteration 0's aggregation MLP)
       const auto& a = fp.st[s].a;
@@ -2376,13 +2483,27 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
       if (!a.masking) wm = a.mcs_mask ? a.mcs_mask[((size_t)b * U + u) * a.M + s] : (s == 0 ? 1.f : 0.f);
       if (!GEN || s == ninit - 1) init_user<P, A2P, 16, TAIL_AGG>(fp.st[s], smem, b, u, strip, wm, s == 0, -1, 0, 0, &fn);
       else if constexpr (GEN) init_user<P, A2P, 16, TAIL_NONE>(fp.st[s], smem, b, u, strip, wm, s == 0, -1, 0, 0, &fn);
+    } else if (GEN && kd == 2) {
+      // U > 4: the leave-one-out combine of the slot's strip rows, in place (k_combine's pass)
+      if constexpr (GEN) combine_item<P>(fp.st[ps], b, strip, &fn);
+    } else if (GEN && !fp_arg.gz) {
+      // U > 2 (or a workspace beyond GZ's 32-bit offsets): the z image is staged in the strip
+      // image by update_user, as in the three-launch forward -- U = 3, 4 with the inline
+      // leave-one-out combine of the U - 1 other users' act*sp rows, U > 4 from the combined
+      // a_u plane (combine stage)
+      if constexpr (GEN) {
+        if (ps < nst - 1) update_user<P, CHP, TAIL_AGG>(fp.st[ps], smem, b, u, strip, &fn, psig);
+        else if (fp_arg.heads_x) update_user<P, CHP, TAIL_READOUT>(fp.st[ps], smem, b, u, strip, &fn, psig);
+        else update_user<P, CHP, TAIL_READOUT_WB>(fp.st[ps], smem, b, u, strip, &fn, psig);
+      }
+      psig = nullptr;
     } else {
       const int fs = strip * P::FO - kHalo;
       if (!pads_zero) zero_pad_symbols<P>(X);   // first item of the workgroup
-      if (s < nst - 1) gz_item_run<P, CHP, TAIL_AGG>(fp.st[s], X, WB, b, u, fs, &fn, psig);
+      if (ps < nst - 1) gz_item_run<P, CHP, TAIL_AGG>(fp.st[ps], X, WB, b, u, fs, &fn, psig);
       else if (GEN && fp_arg.heads_x) {
-        if constexpr (GEN) gz_item_run<P, CHP, TAIL_READOUT>(fp.st[s], X, WB, b, u, fs, &fn, psig);
-      } else gz_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[s], X, WB, b, u, fs, &fn, psig);
+        if constexpr (GEN) gz_item_run<P, CHP, TAIL_READOUT>(fp.st[ps], X, WB, b, u, fs, &fn, psig);
+      } else gz_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[ps], X, WB, b, u, fs, &fn, psig);
       psig = nullptr;
     }
     fstamp(5);
@@ -2396,7 +2517,7 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
     psig = done + s * B + b;
     // a readout item with its heads in the strip image (TAIL_READOUT, H > 1) overwrote the pad
     // symbols: the next item zeroes them again
-    pads_zero = !(GEN && s == nst - 1 && fp_arg.heads_x);
+    pads_zero = !(GEN && kd == 1 && ps == nst - 1 && fp_arg.heads_x);
     j = jn;
     jn = sh[1];
   }
@@ -2414,11 +2535,11 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
   if (sh[3]) {
     // every item ran (a queue whose XCD never received a workgroup would leave its slots
     // undone: error word 2), then the reset
-    for (int i = nrx_tid(); i < nst * B; i += 512)
-      if (__hip_atomic_load(done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ips)
+    for (int i = nrx_tid(); i < nls * B; i += 512)
+      if (__hip_atomic_load(done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ips_of(i / B))
         __hip_atomic_fetch_or(&sy->err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    for (int i = nrx_tid(); i < nst * B; i += 512) done[i] = 0;
+    for (int i = nrx_tid(); i < nls * B; i += 512) done[i] = 0;
     if (nrx_tid() < 8) sy->head[nrx_tid()] = 0;
     if (nrx_tid() == 0) sy->exits = 0;
   }
@@ -2622,12 +2743,23 @@ static int xcc_count() {
   return g_xcc_count[dev];
 }
 
-// k_forward covers the bench-type models: U <= 2 (z images are LDS-DMA copies), one StateInit
-// (no Var-IO mix), one LLR head whose readout fits the paired-readout WB layout, 2A <= 16, at
-// most kFusedMaxStages - 1 iterations; 24-row strips with at least two items per CU (the
-// small-grid tiers keep the three launches: through k_forward they were slower for batch-1
-// latency, profiles/r03/ab_fused_small_latency.txt); a device whose XCDs hold equal CU counts
-// (1..8 XCDs, the queue is picked by the hardware XCC id).
+// k_forward covers: U <= 8 (U <= 2 with a workspace under 1 GB: conv1 reads z from memory, GZ;
+// otherwise the z image is staged in LDS, U = 3, 4 with the inline leave-one-out combine),
+// 1..M StateInit stages (Var-IO), up to three LLR heads,
+// 2A <= 32, num_init + num_it <= kFusedMaxStages; 24-row strips with at least two items per
+// CU (the small-grid tiers keep the three launches: through k_forward they were slower for
+// batch-1 latency, profiles/r03/ab_fused_small_latency.txt); a device whose XCDs hold equal CU
+// counts (1..8 XCDs, the queue is picked by the hardware XCC id).  U = 5..8: a combine stage
+// (k_combine's f32 pass, one item per (slot, strip)) before each update, whose z image then
+// takes the combined a_u plane.
+// one LLR head whose readout fits the paired-readout WB layout (TAIL_READOUT_WB)
+template <class P>
+static bool heads_in_wb(const FwdArgs<_Float16, float, _Float16>& a) {
+  const int chp = 2 * a.A <= 16 ? 16 : 32;
+  return a.H == 1 && heads_fit_wb(a.bits_max, chp, 2 * a.A) &&
+         strip_slots<P>() * slot_pitch<P>() + kHW2 + 256 * (a.bits_max + chp) <= fused_lds<P>();
+}
+
 template <class P>
 static bool fused_applicable(const FwdArgs<_Float16, float, _Float16>& a, int num_it, const FusedCtl& fc) {
   if (!fc.sync || !fc.enabled) return false;
@@ -2636,11 +2768,10 @@ static bool fused_applicable(const FwdArgs<_Float16, float, _Float16>& a, int nu
   const long items = (long)a.B * a.U * ((a.F + P::FO - 1) / P::FO);
   // readout heads: one LLR head in WB (TAIL_READOUT_WB), or up to three + ChEst in the strip
   // image (TAIL_READOUT, X layout)
-  const bool heads = a.H == 1 ? heads_fit_wb(a.bits_max, 16, 2 * a.A) &&
-                                    strip_slots<P>() * slot_pitch<P>() + kHW2 + 256 * (a.bits_max + 16) <= fused_lds<P>()
-                              : a.H <= 3 && (a.H + 1) * (kHeadSlot + 1024) <= strip_slots<P>() * slot_pitch<P>();
-  return items >= 2L * cus && a.ws_bytes < kGzOob && a.pe16 && a.U <= 2 && a.num_init + num_it <= kFusedMaxStages &&
-         2 * a.A <= 16 && a.B <= kFusedMaxB && a.bits_max <= 16 && heads;
+  const bool heads = heads_in_wb<P>(a) || (a.H <= 3 && (a.H + 1) * (kHeadSlot + 1024) <= strip_slots<P>() * slot_pitch<P>());
+  const int nls = a.num_init + num_it * (a.U > kInlineUsers ? 2 : 1);
+  return items >= 2L * cus && a.U <= 8 && a.num_init + num_it <= kFusedMaxStages &&
+         nls <= kFusedMaxLS && 2 * a.A <= 32 && a.B <= kFusedMaxB && a.bits_max <= 16 && heads;
 }
 
 template <class P>
@@ -2650,7 +2781,22 @@ static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, cons
   fp.sync = reinterpret_cast<FusedSync*>(fc.sync);
   fp.ninit = args.num_init;
   fp.nst = args.num_init + num_it;
-  fp.heads_x = args.H > 1;
+  fp.heads_x = !heads_in_wb<P>(args);
+  fp.gz = args.U <= 2 && args.ws_bytes < kGzOob && args.pe16;
+  const bool comb = args.U > kInlineUsers;
+  fp.nls = 0;
+  for (int s = 0; s < fp.ninit; ++s) {
+    fp.kind[fp.nls] = 0;
+    fp.pidx[fp.nls++] = s;
+  }
+  for (int i = 0; i < num_it; ++i) {
+    if (comb) {
+      fp.kind[fp.nls] = 2;
+      fp.pidx[fp.nls++] = fp.ninit + i;
+    }
+    fp.kind[fp.nls] = 1;
+    fp.pidx[fp.nls++] = fp.ninit + i;
+  }
   const int cus = cu_count();
   fp.nq = xcc_count();
   fp.spin_limit = fc.spin_limit;
@@ -2667,7 +2813,7 @@ static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, cons
   FwdArgs<_Float16, float, _Float16> a = args;
   for (int s = 0; s < fp.nst; ++s) {
     BlockParams<P>& bp = fp.st[s];
-    bp.inline_combine = 1;
+    bp.inline_combine = comb ? 0 : 1;   // U > 4: the combine stages write a_u in place
     bp.pair = 0;
     bp.order_rev = 0;
     bp.norm_pre = norm_pre;
@@ -2710,8 +2856,10 @@ static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, cons
   }
 #endif
   B_(K_FUSED);
-  const bool gen = fp.ninit > 1 || fp.heads_x;
-  if (2 * args.A <= 8) {
+  const bool gen = fp.ninit > 1 || fp.heads_x || !fp.gz;
+  if (2 * args.A > 16) {
+    k_forward<P, 32, 32, true><<<cus, 512, L, st>>>(fp);
+  } else if (2 * args.A <= 8) {
     if (gen) k_forward<P, 8, 16, true><<<cus, 512, L, st>>>(fp);
     else k_forward<P, 8, 16, false><<<cus, 512, L, st>>>(fp);
   } else {
@@ -2774,6 +2922,7 @@ hipError_t setup_kernels() {
   set_fused((const void*)k_forward<P16, 16, 16, false>, fused_lds<P16>());
   set_fused((const void*)k_forward<P16, 8, 16, true>, fused_lds<P16>());
   set_fused((const void*)k_forward<P16, 16, 16, true>, fused_lds<P16>());
+  set_fused((const void*)k_forward<P16, 32, 32, true>, fused_lds<P16>());
   return e != hipSuccess ? e : (e1 != hipSuccess ? e1 : e2);
 }
 

@@ -5,7 +5,8 @@ Every configuration of BASELINE.json runs here at the size the bench runs it per
 budget), and the HIP output is compared with the fp64 numpy oracle
 (``oracle/cgnn_ref.cgnn_forward``, semantics neural_rx.py:544-595).  So the launch paths
 the bench takes -- paired aggregation-tail items, paired readout items with the heads in
-WB, Var-IO heads, the k_norm pass and the k_combine pass for U > 4 -- are checked
+WB, Var-IO heads, the k_norm pass, the one-launch forward with its U = 4 z images and U > 4
+combine stages -- are checked
 against the oracle directly, not only for self-consistency.
 
 Tolerances are the ones of tests/test_gpu_parity.py:
@@ -66,10 +67,12 @@ def test_cfg2_random_activity_b128():
 
 def test_cfg4_var_io_random_mcs_b128():
     # BASELINE configs[3] per-GPU shard (1024 / 8): Var-IO with a random one-hot MCS per
-    # (slot, user) over {QPSK, 16-QAM}: two StateInit launches, two LLR heads
+    # (slot, user) over {QPSK, 16-QAM}: two StateInit stages, two LLR heads (k_forward)
     rng = np.random.default_rng(24)
     mcs = rng.integers(0, 2, size=(128, 2))
-    check(make_case("nrx_rt_var_mcs", batch=128, users=2, prbs=4, snr_db=12, seed=24, mcs_choice=mcs))
+    case = make_case("nrx_rt_var_mcs", batch=128, users=2, prbs=4, snr_db=12, seed=24, mcs_choice=mcs)
+    assert took_fused(case)
+    check(case)
 
 
 def test_cfg4b_masking_64qam_b32():
@@ -81,16 +84,30 @@ def test_cfg4b_masking_64qam_b32():
                     mcs_choice=mcs))
 
 
+def took_fused(case) -> bool:
+    eng = engine_for(case)
+    eng.profile(True)
+    run_engine(case, "f16", eng)
+    prof = eng.profile_read()
+    eng.profile(False)
+    return prof["forward"][0] == 1
+
+
 def test_cfg3_full_slot_132prb_16ant_4ue():
     # BASELINE configs[2] topology at full width: 132 PRB (F = 1584), 16 rx antennas
     # (StateInit in-ch 66, ChEst out 32), 4 users, nrx_large (8 iterations); seeded weights
-    # (no trained 16-antenna model exists), one slot; the k_norm pass runs (large grid)
-    case = make_case("nrx_large", batch=1, users=4, prbs=132, num_rx_ant=16, seeded_weights=True,
+    # (no trained 16-antenna model exists); the k_norm pass runs (large grid).  Two slots:
+    # 2 x 4 x 66 = 528 items, so the one-launch forward runs it (U = 4: z images with the
+    # inline leave-one-out combine, ChEst head in the strip image)
+    case = make_case("nrx_large", batch=2, users=4, prbs=132, num_rx_ant=16, seeded_weights=True,
                      random_inputs=True, seed=26)
+    assert took_fused(case)
     check(case)
 
 
 def test_cfg5_full_slot_273prb_8ue_64qam():
-    # BASELINE configs[4] at full width: 273 PRB (F = 3276), 8 users (U > 4: k_combine),
-    # 64-QAM, nrx_large_64qam (8 iterations), one slot
-    check(make_case("nrx_large_64qam", batch=1, users=8, prbs=273, snr_db=25, seed=27))
+    # BASELINE configs[4] at full width: 273 PRB (F = 3276), 8 users (U > 4: combine stages),
+    # 64-QAM, nrx_large_64qam (8 iterations), one slot: 8 x 137 = 1096 items, k_forward
+    case = make_case("nrx_large_64qam", batch=1, users=8, prbs=273, snr_db=25, seed=27)
+    assert took_fused(case)
+    check(case)

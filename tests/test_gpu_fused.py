@@ -5,7 +5,9 @@ work queues with cross-workgroup dependency counters, so 
 must equal the three-launch path bit for bit (``fused_config(enable=False)`` selects that
 path per handle).  The oracle comparison of the same launch shape is tests/test_gpu_baseline_shapes.py
 (cfg2, B = 128, which takes k_forward by default).  Covered here: the bench shape, inactive
-users, U = 1, num_it = 1 (StateInit straight into the readout stage), repeated forwards (the
+users, U = 1, U = 3 / 4 (z images with the inline combine), U = 8 (combine stages), 16
+antennas, Var-IO, 8 iterations, num_it = 1 (StateInit straight into the readout stage),
+repeated forwards (the
 counters are reset by the last workgroup of each launch), a hipGraph replay, the sticky
 timeout word staying 0, that an error word reaches the caller (CGNNEngine.check, sim_ber) and
 that a second stream is refused while the first still runs.
@@ -75,6 +77,29 @@ def test_fused_var_io_identical():
     rng = np.random.default_rng(39)
     mcs = rng.integers(0, 2, size=(128, 2))
     _check_identical(make_case("nrx_rt_var_mcs", batch=128, users=2, prbs=4, snr_db=12, seed=39, mcs_choice=mcs))
+
+
+def test_fused_four_users_16_antennas_identical():
+    # cfg3's topology at a small width: U = 4 (z images with the inline leave-one-out combine
+    # of three planes), 16 antennas (StateInit K = 66, ChEst head of 32 outputs in the strip
+    # image), 8 iterations, seeded weights, some users inactive
+    rng = np.random.default_rng(40)
+    active = (rng.random((64, 4)) < 0.8).astype(np.float32)
+    _check_identical(make_case("nrx_large", batch=64, users=4, prbs=4, num_rx_ant=16, seeded_weights=True,
+                               random_inputs=True, seed=40, active=active))
+
+
+def test_fused_eight_users_combine_identical():
+    # cfg5's user count: U = 8 > 4, so a combine stage (k_combine's pass, one item per (slot,
+    # strip)) runs before every update and conv1 reads the combined a_u planes; 64-QAM,
+    # 8 iterations, some users inactive
+    rng = np.random.default_rng(42)
+    active = (rng.random((32, 8)) < 0.8).astype(np.float32)
+    _check_identical(make_case("nrx_large_64qam", batch=32, users=8, prbs=4, snr_db=20, seed=42, active=active))
+
+
+def test_fused_three_users_identical():
+    _check_identical(make_case("nrx_rt", batch=96, users=3, prbs=4, snr_db=12, seed=41))
 
 
 def test_fused_8_iterations_identical():

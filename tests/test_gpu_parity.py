@@ -31,9 +31,15 @@ F16_FLIP_CONF_TOL = 1e-3
 _engines = {}
 
 
+def _weights_key(ws):
+    # content fingerprint: two seeded weight sets of one spec must not share an engine
+    return tuple((np.shape(w), float(np.asarray(w, np.float64).ravel()[:16].sum())) for w in ws)
+
+
 def engine_for(case):
+    """One engine per (model, spec, weight set)."""
     from neural_rx_amd.receiver import CGNNEngine
-    key = (case.name, case.spec, id(case.weights) if case.name == "seeded" else 0)
+    key = (case.name, case.spec, _weights_key(case.weights))
     if key not in _engines:
         _engines[key] = CGNNEngine(case.spec, case.weights)
     return _engines[key]
