@@ -302,12 +302,15 @@ int nrx_profile_read(nrx_handle* h, int32_t kernel, int64_t* launches, double* t
  * Forwards on one handle must not run concurrently on several streams (the counters are per
  * handle): nrx_forward returns NRX_ERR_BUSY when a forward that would take this path arrives
  * on a stream other than the previous forward's while that stream still has work pending.
- * NRX_FUSED=0 in the environment (read by nrx_create) takes the three-launch path instead. */
+ * NRX_FUSED=0 in the environment (read by nrx_create) takes the three-launch path instead, 2
+ * the one-launch forward wherever it applies. */
 int nrx_fused_status(nrx_handle* h, int32_t* status, int32_t reset);
 
-/* Per-handle control of the one-launch forward: enable = 1 / 0 takes it (when applicable) or
- * the three-launch path (< 0: unchanged; the initial value comes from NRX_FUSED at
- * nrx_create); spin_limit = dependency-wait polls before the timeout error (<= 0: the
+/* Per-handle control of the one-launch forward: enable = 0 the three-launch path; 1 (default)
+ * the one-launch forward for the shapes it is measured faster on (one StateInit, one LLR head,
+ * U <= 2); 2 for every shape it applies to (Var-IO, several heads, U <= 8, 2A <= 32; outputs
+ * identical to the three launches); < 0: unchanged.  The initial value comes from NRX_FUSED
+ * (0 / 1 / 2) at nrx_create; spin_limit = dependency-wait polls before the timeout error (<= 0: the
  * default, ~0.5 s); inject_err = error bits the next forwards set in the error word (test
  * hook: callers must surface them; 0: none). */
 int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t inject_err);

@@ -350,7 +350,7 @@ struct nrx_handle {
   DeviceModel<double, double> m64;
   EventProf* prof = nullptr;
   void* fused_sync = nullptr;   // k_forward's work queues and dependency counters (zeroed)
-  bool fused_enabled = true;    // NRX_FUSED (environment, read once at nrx_create)
+  int fused_enabled = 1;    // NRX_FUSED (environment, read once at nrx_create)
   int spin_limit = kFusedSpinLimit;
   int dbg_err = 0;
   hipStream_t last_stream = nullptr;   // stream of the last one-launch forward
@@ -457,7 +457,8 @@ int nrx_create(const nrx_desc* desc, const float* const* weights, const int64_t*
   h->device = device;
   {
     const char* ev = getenv("NRX_FUSED");   // A/B and bit-identity tests: 0 = three launches
-    h->fused_enabled = !ev || atoi(ev) != 0;
+    h->fused_enabled = ev ? atoi(ev) : 1;
+    if (h->fused_enabled < 0 || h->fused_enabled > 2) h->fused_enabled = 1;
   }
   e = hipMalloc(&h->fused_sync, fused_sync_bytes());
   if (e == hipSuccess) e = hipMemset(h->fused_sync, 0, fused_sync_bytes());
@@ -789,7 +790,7 @@ int nrx_fused_status(nrx_handle* h, int32_t* status, int32_t reset) {
 
 int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t inject_err) {
   if (!h) return fail(NRX_ERR_INVALID_ARG, "null argument");
-  if (enable >= 0) h->fused_enabled = enable != 0;
+  if (enable >= 0) h->fused_enabled = enable > 2 ? 2 : enable;
   h->spin_limit = spin_limit > 0 ? spin_limit : kFusedSpinLimit;
   h->dbg_err = inject_err;
   return NRX_OK;

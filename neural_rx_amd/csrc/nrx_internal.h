@@ -111,7 +111,7 @@ struct FwdArgs {
 // the dependency-wait bound and debug error bits (nrx_debug_fused).
 struct FusedCtl {
   void* sync;
-  bool enabled;
+  int enabled;   // 0 off, 1 where measured faster (the bench-type schedule), 2 every applicable shape
   int spin_limit;
   int dbg_err;
 };

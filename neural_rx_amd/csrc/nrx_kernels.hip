@@ -2316,6 +2316,7 @@ __device__ __forceinline__ void fused_wait(const int* cnt, int need, FusedSync* 
 // order, then (sum - sp_u) * p), so the outputs equal the three-launch forward's.  Its rows
 // are its own strip's (no halo); the next update stage waits for all strips of the slot.  It
 // runs no conv2, so the next item's dependency poll is done at its end.
+constexpr int kFusedMaxUsers = 8;
 template <class P>
 __device__ __forceinline__ void combine_item(const BlockParams<P>& prm, int b, int strip, FusedNext<P>* fn) {
   using S = typename P::S;
@@ -2334,18 +2335,26 @@ __device__ __forceinline__ void combine_item(const BlockParams<P>& prm, int b, i
   const int n = (f1 - f0) * kT * QS;
   for (int idx = nrx_tid(); idx < n; idx += 512) {
     S* base = buf + (size_t)(idx / QS) * kDS + (idx % QS) * P::EPC;
+    // every user's chunk in flight at once (one workgroup per CU: a load-use chain per user
+    // would leave the CU waiting U memory latencies per chunk)
+    intx4 vv[kFusedMaxUsers];
+#pragma unroll
+    for (int uu = 0; uu < kFusedMaxUsers; ++uu)
+      vv[uu] = uu < U ? *reinterpret_cast<const intx4*>(base + uu * ustride) : intx4{0, 0, 0, 0};
     Real sum[P::EPC];
 #pragma unroll
     for (int e = 0; e < P::EPC; ++e) sum[e] = 0;
-    for (int uu = 0; uu < U; ++uu) {
-      const intx4 v = *reinterpret_cast<const intx4*>(base + uu * ustride);
-      const S* sv = reinterpret_cast<const S*>(&v);
+#pragma unroll
+    for (int uu = 0; uu < kFusedMaxUsers; ++uu) {
+      if (uu >= U) break;
+      const S* sv = reinterpret_cast<const S*>(&vv[uu]);
 #pragma unroll
       for (int e = 0; e < P::EPC; ++e) sum[e] += (Real)sv[e];
     }
-    for (int uu = 0; uu < U; ++uu) {
-      const intx4 v = *reinterpret_cast<const intx4*>(base + uu * ustride);
-      const S* sv = reinterpret_cast<const S*>(&v);
+#pragma unroll
+    for (int uu = 0; uu < kFusedMaxUsers; ++uu) {
+      if (uu >= U) break;
+      const S* sv = reinterpret_cast<const S*>(&vv[uu]);
       S o[P::EPC];
 #pragma unroll
       // rounded to f32 before the storage conversion (as k_combine: no fused single-rounding
@@ -2365,11 +2374,15 @@ __device__ __forceinline__ void combine_item(const BlockParams<P>& prm, int b, i
   }
 }
 
-// GEN: the general stage list (Var-IO StateInit stages, readout heads in the strip image);
-// the plain kernel keeps only the one-StateInit / one-head code (its code size -- 141 KB
-// against 237 KB -- measured 3.5 % faster, profiles/r04/ab_fused_gen.txt)
-template <class P, int A2P, int CHP, bool GEN>
+// MODE 0: one StateInit, one head in WB, GZ updates (the bench shape); 1: the general stage
+// list with GZ updates (Var-IO StateInit stages, readout heads in the strip image); 2: staged
+// z images (U > 2 or a workspace beyond GZ's offsets) with combine stages for U > 4.  Each
+// kernel carries only its own item code: compiling the general list into the bench kernel grew
+// it from 141 KB to 237 KB and cost 3.5 % (profiles/r04/ab_fused_gen.txt).
+template <class P, int A2P, int CHP, int MODE>
 __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
+  constexpr bool GEN = MODE != 0;
+  constexpr bool STAGED = MODE == 2;
   // the stage parameters are read through the kernarg segment pointer: indexing the by-value
   // parameter with the (dynamic) stage made the compiler copy the whole struct to scratch
   typedef const __attribute__((address_space(4))) FusedParams<P> KFP;
@@ -2483,27 +2496,29 @@ __global__ __launch_bounds__(512) void k_forward(FusedParams<P> fp_arg) {
       if (!a.masking) wm = a.mcs_mask ? a.mcs_mask[((size_t)b * U + u) * a.M + s] : (s == 0 ? 1.f : 0.f);
       if (!GEN || s == ninit - 1) init_user<P, A2P, 16, TAIL_AGG>(fp.st[s], smem, b, u, strip, wm, s == 0, -1, 0, 0, &fn);
       else if constexpr (GEN) init_user<P, A2P, 16, TAIL_NONE>(fp.st[s], smem, b, u, strip, wm, s == 0, -1, 0, 0, &fn);
-    } else if (GEN && kd == 2) {
+    } else if (STAGED && kd == 2) {
       // U > 4: the leave-one-out combine of the slot's strip rows, in place (k_combine's pass)
-      if constexpr (GEN) combine_item<P>(fp.st[ps], b, strip, &fn);
-    } else if (GEN && !fp_arg.gz) {
+      if constexpr (STAGED) combine_item<P>(fp.st[ps], b, strip, &fn);
+    } else if (STAGED) {
       // U > 2 (or a workspace beyond GZ's 32-bit offsets): the z image is staged in the strip
       // image by update_user, as in the three-launch forward -- U = 3, 4 with the inline
       // leave-one-out combine of the U - 1 other users' act*sp rows, U > 4 from the combined
       // a_u plane (combine stage)
-      if constexpr (GEN) {
+      if constexpr (STAGED) {
         if (ps < nst - 1) update_user<P, CHP, TAIL_AGG>(fp.st[ps], smem, b, u, strip, &fn, psig);
         else if (fp_arg.heads_x) update_user<P, CHP, TAIL_READOUT>(fp.st[ps], smem, b, u, strip, &fn, psig);
         else update_user<P, CHP, TAIL_READOUT_WB>(fp.st[ps], smem, b, u, strip, &fn, psig);
       }
       psig = nullptr;
     } else {
-      const int fs = strip * P::FO - kHalo;
-      if (!pads_zero) zero_pad_symbols<P>(X);   // first item of the workgroup
-      if (ps < nst - 1) gz_item_run<P, CHP, TAIL_AGG>(fp.st[ps], X, WB, b, u, fs, &fn, psig);
-      else if (GEN && fp_arg.heads_x) {
-        if constexpr (GEN) gz_item_run<P, CHP, TAIL_READOUT>(fp.st[ps], X, WB, b, u, fs, &fn, psig);
-      } else gz_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[ps], X, WB, b, u, fs, &fn, psig);
+      if constexpr (!STAGED) {
+        const int fs = strip * P::FO - kHalo;
+        if (!pads_zero) zero_pad_symbols<P>(X);   // first item of the workgroup
+        if (ps < nst - 1) gz_item_run<P, CHP, TAIL_AGG>(fp.st[ps], X, WB, b, u, fs, &fn, psig);
+        else if (GEN && fp_arg.heads_x) {
+          if constexpr (GEN) gz_item_run<P, CHP, TAIL_READOUT>(fp.st[ps], X, WB, b, u, fs, &fn, psig);
+        } else gz_item_run<P, CHP, TAIL_READOUT_WB>(fp.st[ps], X, WB, b, u, fs, &fn, psig);
+      }
       psig = nullptr;
     }
     fstamp(5);
@@ -2761,6 +2776,15 @@ static bool heads_in_wb(const FwdArgs<_Float16, float, _Float16>& a) {
 }
 
 template <class P>
+static bool fused_gz(const FwdArgs<_Float16, float, _Float16>& a) {
+  return a.U <= 2 && a.ws_bytes < kGzOob && a.pe16;
+}
+template <class P>
+static int fused_mode(const FwdArgs<_Float16, float, _Float16>& a) {
+  return !fused_gz<P>(a) ? 2 : (a.num_init > 1 || !heads_in_wb<P>(a) ? 1 : 0);
+}
+
+template <class P>
 static bool fused_applicable(const FwdArgs<_Float16, float, _Float16>& a, int num_it, const FusedCtl& fc) {
   if (!fc.sync || !fc.enabled) return false;
   const int cus = cu_count(), nx = xcc_count();
@@ -2770,7 +2794,10 @@ static bool fused_applicable(const FwdArgs<_Float16, float, _Float16>& a, int nu
   // image (TAIL_READOUT, X layout)
   const bool heads = heads_in_wb<P>(a) || (a.H <= 3 && (a.H + 1) * (kHeadSlot + 1024) <= strip_slots<P>() * slot_pitch<P>());
   const int nls = a.num_init + num_it * (a.U > kInlineUsers ? 2 : 1);
-  return items >= 2L * cus && a.U <= 8 && a.num_init + num_it <= kFusedMaxStages &&
+  // the default (enabled == 1) takes only the bench-type schedule (MODE 0): the general and
+  // staged-z kernels measured slower than the three launches
+  if (fc.enabled == 1 && fused_mode<P>(a) != 0) return false;
+  return items >= 2L * cus && a.U <= kFusedMaxUsers && a.num_init + num_it <= kFusedMaxStages &&
          nls <= kFusedMaxLS && 2 * a.A <= 32 && a.B <= kFusedMaxB && a.bits_max <= 16 && heads;
 }
 
@@ -2782,7 +2809,7 @@ static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, cons
   fp.ninit = args.num_init;
   fp.nst = args.num_init + num_it;
   fp.heads_x = !heads_in_wb<P>(args);
-  fp.gz = args.U <= 2 && args.ws_bytes < kGzOob && args.pe16;
+  fp.gz = fused_gz<P>(args);
   const bool comb = args.U > kInlineUsers;
   fp.nls = 0;
   for (int s = 0; s < fp.ninit; ++s) {
@@ -2856,15 +2883,18 @@ static hipError_t run_fused(const FwdArgs<_Float16, float, _Float16>& args, cons
   }
 #endif
   B_(K_FUSED);
-  const bool gen = fp.ninit > 1 || fp.heads_x || !fp.gz;
+  const int mode = fused_mode<P>(args);
   if (2 * args.A > 16) {
-    k_forward<P, 32, 32, true><<<cus, 512, L, st>>>(fp);
+    if (mode == 2) k_forward<P, 32, 32, 2><<<cus, 512, L, st>>>(fp);
+    else k_forward<P, 32, 32, 1><<<cus, 512, L, st>>>(fp);
   } else if (2 * args.A <= 8) {
-    if (gen) k_forward<P, 8, 16, true><<<cus, 512, L, st>>>(fp);
-    else k_forward<P, 8, 16, false><<<cus, 512, L, st>>>(fp);
+    if (mode == 2) k_forward<P, 8, 16, 2><<<cus, 512, L, st>>>(fp);
+    else if (mode == 1) k_forward<P, 8, 16, 1><<<cus, 512, L, st>>>(fp);
+    else k_forward<P, 8, 16, 0><<<cus, 512, L, st>>>(fp);
   } else {
-    if (gen) k_forward<P, 16, 16, true><<<cus, 512, L, st>>>(fp);
-    else k_forward<P, 16, 16, false><<<cus, 512, L, st>>>(fp);
+    if (mode == 2) k_forward<P, 16, 16, 2><<<cus, 512, L, st>>>(fp);
+    else if (mode == 1) k_forward<P, 16, 16, 1><<<cus, 512, L, st>>>(fp);
+    else k_forward<P, 16, 16, 0><<<cus, 512, L, st>>>(fp);
   }
   E_(K_FUSED);
   return hipGetLastError();
@@ -2918,11 +2948,14 @@ hipError_t setup_kernels() {
     hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (r != hipSuccess && e2 == hipSuccess) e2 = r;
   };
-  set_fused((const void*)k_forward<P16, 8, 16, false>, fused_lds<P16>());
-  set_fused((const void*)k_forward<P16, 16, 16, false>, fused_lds<P16>());
-  set_fused((const void*)k_forward<P16, 8, 16, true>, fused_lds<P16>());
-  set_fused((const void*)k_forward<P16, 16, 16, true>, fused_lds<P16>());
-  set_fused((const void*)k_forward<P16, 32, 32, true>, fused_lds<P16>());
+  set_fused((const void*)k_forward<P16, 8, 16, 0>, fused_lds<P16>());
+  set_fused((const void*)k_forward<P16, 16, 16, 0>, fused_lds<P16>());
+  set_fused((const void*)k_forward<P16, 8, 16, 1>, fused_lds<P16>());
+  set_fused((const void*)k_forward<P16, 16, 16, 1>, fused_lds<P16>());
+  set_fused((const void*)k_forward<P16, 8, 16, 2>, fused_lds<P16>());
+  set_fused((const void*)k_forward<P16, 16, 16, 2>, fused_lds<P16>());
+  set_fused((const void*)k_forward<P16, 32, 32, 1>, fused_lds<P16>());
+  set_fused((const void*)k_forward<P16, 32, 32, 2>, fused_lds<P16>());
   return e != hipSuccess ? e : (e1 != hipSuccess ? e1 : e2);
 }
 

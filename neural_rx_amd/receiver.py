@@ -111,11 +111,12 @@ class CGNNEngine:
         st = (ctypes.c_int32 * 3)()
         _lib.check(self._lib.nrx_fused_status(self._h, st, 1))
 
-    def fused_config(self, enable: Optional[bool] = None, spin_limit: int = 0, inject_err: int = 0):
-        """One-launch forward control (include/nrx.h nrx_fused_config): ``enable`` True/False
-        (None: unchanged), the dependency-wait bound (<= 0: default) and error bits to inject
-        (test hook)."""
-        en = -1 if enable is None else int(bool(enable))
+    def fused_config(self, enable=None, spin_limit: int = 0, inject_err: int = 0):
+        """One-launch forward control (include/nrx.h nrx_fused_config): ``enable`` False / True
+        (where it is the faster schedule) / "force" (every shape it applies to), None:
+        unchanged; the dependency-wait bound (<= 0: default) and error bits to inject (test
+        hook)."""
+        en = -1 if enable is None else (2 if enable == "force" else int(bool(enable)))
         _lib.check(self._lib.nrx_fused_config(self._h, en, int(spin_limit), int(inject_err)))
 
     def profile_read(self):

@@ -23,8 +23,10 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(case, fused: bool):
+    # fused: every shape the one-launch forward applies to ("force"; the default takes it only
+    # for the bench-type schedule, where it is the faster one)
     eng = engine_for(case)
-    eng.fused_config(enable=fused)
+    eng.fused_config(enable="force" if fused else False)
     try:
         return run_engine(case, "f16", eng)
     finally:
