@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NRX_API_VERSION 5
+#define NRX_API_VERSION 6
 
 enum nrx_status {
   NRX_OK = 0,

@@ -1404,7 +1404,7 @@ template <class P, int CINP, int CHP, int TAILM, bool GZIN = false>
 __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, char* WB, int b, int u,
                                             int f_start, int mode, typename P::Real wm, bool first, int nb = -1,
                                             int nu = 0, int nfs = 0, FusedNext<P>* fn = nullptr,
-                                            const GZ* gz = nullptr) {
+                                            const GZ* gz = nullptr, int* psig = nullptr) {
   constexpr int R0 = strip_slots<P>();
   const int F = prm.a.F;
   // fused forward: dequeue the item after next here, past the item's prologue waits (an
@@ -1420,8 +1420,12 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
         if constexpr (!kPrefetchW) nx.load(prm.w[1]);
         nx.store(WB);
       }
+      // k_forward GZ items: the previous item's stores are drained here, where every wave has
+      // consumed its loads anyway, and its counter is added after the layer barrier
+      if (psig) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }, gz);
   }
+  if (psig && nrx_tid() == 0) __hip_atomic_fetch_add(psig, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp(2);
   {
     SepStage<kHID, kDSP> nx;
@@ -1920,14 +1924,13 @@ __device__ __forceinline__ void gz_item_run(const BlockParams<P>& prm, char* X, 
 #pragma unroll
     for (int i = 0; i < 6; ++i) gz.x0[i] = (i < 5 || wave < 4) ? gz.load(0, gz.row_soff(p0 - 1 + i)) : half8{};
   }
-  // the previous item's stores drain behind these loads; its counter is added once every
-  // wave has drained (deferred signal, k_forward)
-  if (psig) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the previous item's stores drain during conv1 and its counter is added after conv1's
+  // layer barrier (deferred signal, k_forward): the prologue waits for the conv1 weights only,
+  // the z-row loads stay in flight across the barrier
   w1.store(WB);
   __syncthreads();
-  if (psig && nrx_tid() == 0) __hip_atomic_fetch_add(psig, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp(1);
-  strip_block<P, kUPD_CINP, CHP, TAILM, true>(prm, X, WB, b, u, f_start, 0, 0, false, -1, 0, 0, fn, &gz);
+  strip_block<P, kUPD_CINP, CHP, TAILM, true>(prm, X, WB, b, u, f_start, 0, 0, false, -1, 0, 0, fn, &gz, psig);
   stamp(4);
 }
 
