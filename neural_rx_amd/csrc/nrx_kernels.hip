@@ -594,7 +594,7 @@ __device__ __forceinline__ void conv_rows(const char* X, int s0, int nslots, int
 // the same barriers.
 template <class P, int CINP, int COUTP, int R, bool GZIN, class WS, class Epi, class Post>
 __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off, int p0, bool act, bool first_round,
-                                           const WS& ws, Epi& epi, Post& post_math, const GZ* gz) {
+                                           const WS& ws, Epi& epi, Post& post_math, const GZ* gz, bool skip = false) {
   using E = std::decay_t<Epi>;
   const int lane = nrx_tid() & 63;
   const int t = lane & 15, g = lane >> 4;
@@ -603,7 +603,9 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
   stamp(8 + 5 * in_off);
   if (act) epi.template prefetch<R>(pf, p0, t, g);   // epilogue global loads, in flight during the math
   if (act) {
-    if constexpr (NRX_ABLATE & 1) {
+    if (skip || (NRX_ABLATE & 1)) {
+      // skip: a StateInit_m item whose MCS weight is 0 (its conv output only ever enters as
+      // 0 * finite): no math, any finite accumulator (the bias) gives the same state
 #pragma unroll
       for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -671,7 +673,7 @@ __device__ __forceinline__ void layer_pass(const char* X, int nslots, int in_off
 template <class P, int CINP, int COUTP, bool GZIN = false, class WS, class Epi, class Post>
 __device__ __forceinline__ void conv_layer(const char* X, int nslots, int in_off, int pos_lo,
                                            int pos_hi, const WS& ws, Epi&& epi, Post&& post_math,
-                                           const GZ* gz = nullptr) {
+                                           const GZ* gz = nullptr, bool skip = false) {
   const int wave = __builtin_amdgcn_readfirstlane(nrx_tid() >> 6);
   if constexpr (P::WLDS) {
     static_assert(P::R == 4, "f16 row split assumes passes of 4 / 3 rows");
@@ -680,13 +682,13 @@ __device__ __forceinline__ void conv_layer(const char* X, int nslots, int in_off
     n4 = n4 < 0 ? 0 : n4;
     const int p0 = pos_lo + 4 * (wave < n4 ? wave : n4) + 3 * (wave > n4 ? wave - n4 : 0);
     const bool act = p0 < pos_hi;
-    if (wave < n4) layer_pass<P, CINP, COUTP, 4, GZIN>(X, nslots, in_off, p0, act, true, ws, epi, post_math, gz);
-    else layer_pass<P, CINP, COUTP, 3, GZIN>(X, nslots, in_off, p0, act, true, ws, epi, post_math, gz);
+    if (wave < n4) layer_pass<P, CINP, COUTP, 4, GZIN>(X, nslots, in_off, p0, act, true, ws, epi, post_math, gz, skip);
+    else layer_pass<P, CINP, COUTP, 3, GZIN>(X, nslots, in_off, p0, act, true, ws, epi, post_math, gz, skip);
   } else {
     for (int base = pos_lo; base < pos_hi; base += 8 * P::R) {
       const int p0 = base + wave * P::R;
       layer_pass<P, CINP, COUTP, P::R, false>(X, nslots, in_off, p0, p0 < pos_hi, base == pos_lo, ws, epi, post_math,
-                                              nullptr);
+                                              nullptr, skip);
     }
   }
 }
@@ -882,14 +884,14 @@ __device__ __forceinline__ size_t srow(int b, int u, int f, int t, int U, int F)
 template <class P, int CINP, int COUTP, bool GZIN = false, class Epi, class Post>
 __device__ __forceinline__ void run_layer(char* X, char* WB, const SepW<typename P::WT, typename P::BT>& w,
                                           int in_off, int pos_lo, int pos_hi, Epi&& epi_of, Post&& post,
-                                          const GZ* gz = nullptr) {
+                                          const GZ* gz = nullptr, bool skip = false) {
   constexpr int R0 = strip_slots<P>();
   if constexpr (P::WLDS) {
     WLds<P, CINP, COUTP> ws{WB};
-    conv_layer<P, CINP, COUTP, GZIN>(X, R0, in_off, pos_lo, pos_hi, ws, epi_of(ws), post, gz);
+    conv_layer<P, CINP, COUTP, GZIN>(X, R0, in_off, pos_lo, pos_hi, ws, epi_of(ws), post, gz, skip);
   } else {
     WGlb<P, CINP, COUTP> ws{w};
-    conv_layer<P, CINP, COUTP>(X, R0, in_off, pos_lo, pos_hi, ws, epi_of(ws), post);
+    conv_layer<P, CINP, COUTP>(X, R0, in_off, pos_lo, pos_hi, ws, epi_of(ws), post, nullptr, skip);
   }
 }
 
@@ -1404,13 +1406,17 @@ template <class P, int CINP, int CHP, int TAILM, bool GZIN = false>
 __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, char* WB, int b, int u,
                                             int f_start, int mode, typename P::Real wm, bool first, int nb = -1,
                                             int nu = 0, int nfs = 0, FusedNext<P>* fn = nullptr,
-                                            const GZ* gz = nullptr, int* psig = nullptr) {
+                                            const GZ* gz = nullptr, int* psig = nullptr, bool skip = false) {
   constexpr int R0 = strip_slots<P>();
   const int F = prm.a.F;
   // fused forward: dequeue the item after next here, past the item's prologue waits (an
   // older pending atomic would hold every vmcnt wait of wave 0); read at the item's end
   if (fn && nrx_tid() == 0) fn->jnn = atomicAdd(fn->head, 1);
-  {
+  // skip (StateInit_m with MCS weight 0, f16): conv1 / conv2 are not run at all -- conv3's
+  // weights (and the aggregation MLP) are staged directly and conv3 runs its epilogue on the
+  // bias (0 * finite, like the skipped conv output)
+  const bool fast = P::WLDS && skip;
+  if (!fast) {
     SepStage<kHID, kHID> nx;
     if constexpr (P::WLDS && kPrefetchW) nx.load(prm.w[1]);
     run_layer<P, CINP, kHID, GZIN>(X, WB, prm.w[0], 0, 1, R0 - 1, [&](auto ws) {
@@ -1423,11 +1429,38 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
       // k_forward GZ items: the previous item's stores are drained here, where every wave has
       // consumed its loads anyway, and its counter is added after the layer barrier
       if (psig) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }, gz);
+    }, gz, skip);
   }
   if (psig && nrx_tid() == 0) __hip_atomic_fetch_add(psig, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp(2);
-  {
+  if (fast) {
+    if constexpr (P::WLDS) {
+      SepStage<kHID, kDSP> nx;
+      DenseStage<kDSP, kAGG> d1;
+      DenseStage<kAGG, kDSP> d2;
+      nx.load(prm.w[2]);
+      if constexpr (TAILM == TAIL_AGG) {
+        d1.load(prm.agg[0]);
+        d2.load(prm.agg[1]);
+      }
+      int pv = 0;
+      const bool poll = fn && fn->ndone && nrx_tid() == 0;
+      if (poll) {
+        pv = __hip_atomic_load(fn->ndone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("buffer_inv sc1" ::: "memory");
+      }
+      nx.store(WB);
+      if constexpr (TAILM == TAIL_AGG) {
+        d1.store(WB + 16 * 1024, reinterpret_cast<float*>(WB + kWTailBias));
+        d2.store(WB + 24 * 1024, reinterpret_cast<float*>(WB + kWTailBias + kAGG * 4));
+      }
+      if (poll) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        *fn->nflag = pv >= fn->nneed;
+      }
+      __syncthreads();
+    }
+  } else {
     SepStage<kHID, kDSP> nx;
     DenseStage<kDSP, kAGG> d1;
     DenseStage<kAGG, kDSP> d2;
@@ -1466,7 +1499,7 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
           d2.store(WB + 24 * 1024, reinterpret_cast<float*>(WB + kWTailBias + kAGG * 4));
         }
       }
-    });
+    }, nullptr, skip);
   }
   stamp(3);
   {
@@ -1511,7 +1544,7 @@ __device__ __forceinline__ void strip_block(const BlockParams<P>& prm, char* X, 
         c1.store(X + head_w1(H), reinterpret_cast<float*>(X + head_b1(H)));
         c2.store(X + head_w2(H), reinterpret_cast<float*>(X + head_b2(H)));
       }
-    });
+    }, nullptr, skip);
   }
 }
 
@@ -1637,6 +1670,35 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
       }
     }
   };
+  if (!a.masking && wm == (Real)0) {
+    // Var-IO: this MCS does not apply to (b, u) (one-hot mask), so StateInit_m enters the
+    // state as 0 * finite (neural_rx.py:562-569): no z image, no conv math; the block still
+    // stages its layer weights and runs the epilogue (the first stage writes the zero state,
+    // the last one the aggregation MLP of the accumulated state).  Bit-identical up to the
+    // sign of zero states (the bias replaces the conv output in the 0 * finite product).
+    // The pad symbols are zeroed whatever CINP is (a full item's z image would have).
+    if constexpr (sizeof(S) == 2) {
+      constexpr int NQ = kHID * (int)sizeof(S) / 16;
+      for (int idx = nrx_tid(); idx < R0 * 2 * NQ; idx += 512) {
+        const int q = idx % NQ, tt = kT + (idx / NQ) % 2, lf = idx / (2 * NQ);
+        *reinterpret_cast<intx4*>(X + xoff<P, NQ>(lf, tt, q)) = intx4{0, 0, 0, 0};
+      }
+    }
+    if constexpr (sizeof(S) == 2) {
+      // one-launch forward: the pe16 rows of this item (every other user of the slot may skip too)
+      const int lf = nrx_tid() / kTP, tt = nrx_tid() % kTP, f = f_start + lf;
+      if (fn && a.pe16 && lf >= kHalo && lf < kHalo + P::FO && lf < R0 && tt < kT && f >= 0 && f < F) {
+        const float2 pv = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + f) * kT + tt) * 2);
+        S pe2[8] = {};
+        pe2[0] = (S)pv.x;
+        pe2[1] = (S)pv.y;
+        *reinterpret_cast<intx4*>(a.pe16 + (((size_t)u * F + f) * kT + tt) * kDS) = *reinterpret_cast<const intx4*>(pe2);
+      }
+    }
+    __syncthreads();
+    strip_block<P, CINP, CHP, TAILM>(prm, X, WB, b, u, f_start, 1, wm, first, nb, nu, nfs, fn, nullptr, nullptr, true);
+    return;
+  }
   SepStage<CINP, kHID> w1;
   // NRX_INIT_ORDER: the y / h / pe loads (the norm -> z chain) go out first; the conv1
   // weights and the pad zeroing follow them
@@ -2797,9 +2859,9 @@ static bool fused_applicable(const FwdArgs<_Float16, float, _Float16>& a, int nu
   // image (TAIL_READOUT, X layout)
   const bool heads = heads_in_wb<P>(a) || (a.H <= 3 && (a.H + 1) * (kHeadSlot + 1024) <= strip_slots<P>() * slot_pitch<P>());
   const int nls = a.num_init + num_it * (a.U > kInlineUsers ? 2 : 1);
-  // the default (enabled == 1) takes only the bench-type schedule (MODE 0): the general and
-  // staged-z kernels measured slower than the three launches
-  if (fc.enabled == 1 && fused_mode<P>(a) != 0) return false;
+  // the default (enabled == 1) takes the GZ schedules (MODE 0, 1: cfg2, cfg4, cfg4'); the
+  // staged-z kernel (cfg3, cfg5) measured slower than the three launches
+  if (fc.enabled == 1 && fused_mode<P>(a) == 2) return false;
   return items >= 2L * cus && a.U <= kFusedMaxUsers && a.num_init + num_it <= kFusedMaxStages &&
          nls <= kFusedMaxLS && 2 * a.A <= 32 && a.B <= kFusedMaxB && a.bits_max <= 16 && heads;
 }
