@@ -286,6 +286,8 @@ def main():
     pmc_src = None
     if traffic is not None:
         pmc_src = pmc.get(key, {}).get("source")
+    # three launches: the whole forward's traffic (sum over its launches) beside the per-launch one
+    fwd_traffic = None if fused else pmc.get(key, {}).get("forward_bytes")
     # SQ counters of the dominant kernel from the committed PMC capture (tools/pmc_record.py)
     sq = {}
     sq_path = os.path.join(ROOT, "profiles", "pmc_sq.json")
@@ -302,7 +304,10 @@ def main():
                 "algorithmic_bytes_per_launch": compulsory if fused else None,
                 "algorithmic_bytes_kind": "compulsory I/O of the forward (SURVEY 8(d): y, h_hat in, f32 LLRs "
                                           "and h_ref out, pe once)",
-                "traffic_over_compulsory": round(traffic / compulsory, 3) if (traffic and fused) else None,
+                "traffic_over_compulsory": round(traffic / compulsory, 3) if (traffic and fused) else (
+                    round(fwd_traffic / compulsory, 3) if fwd_traffic else None),
+                "compulsory_bytes_per_forward": compulsory,
+                "traffic_per_forward": traffic if fused else fwd_traffic,
                 "schedule_bytes_per_launch": round(alg_bytes),
                 "schedule_bytes_kind": "the schedule's own hand-offs: StateInit reads y, h_hat and writes s, "
                                        "act*sp; every update reads s, a and writes s', act*sp or the outputs",

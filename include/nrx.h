@@ -308,9 +308,9 @@ int nrx_fused_status(nrx_handle* h, int32_t* status, int32_t reset);
 
 /* Per-handle control of the one-launch forward: enable = 0 the three-launch path; 1 (default)
  * the one-launch forward for the shapes it is measured faster on (U <= 2 with conv1 reading its
- * rows from memory: one or several StateInit stages and heads); 2 for every shape it applies to
- * (also U <= 8 and 2A <= 32 with staged z images; outputs identical to the three launches);
- * < 0: unchanged.  The initial value comes from NRX_FUSED
+ * rows from memory, at least four stages: Var-IO, 8 iterations); 2 for every shape it applies
+ * to (also the 2-iteration bench forward, U <= 8 and 2A <= 32 with staged z images; outputs
+ * identical to the three launches); < 0: unchanged.  The initial value comes from NRX_FUSED
  * (0 / 1 / 2) at nrx_create; spin_limit = dependency-wait polls before the timeout error (<= 0: the
  * default, ~0.5 s); inject_err = error bits the next forwards set in the error word (test
  * hook: callers must surface them; 0: none). */

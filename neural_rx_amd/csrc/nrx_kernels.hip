@@ -2859,9 +2859,11 @@ static bool fused_applicable(const FwdArgs<_Float16, float, _Float16>& a, int nu
   // image (TAIL_READOUT, X layout)
   const bool heads = heads_in_wb<P>(a) || (a.H <= 3 && (a.H + 1) * (kHeadSlot + 1024) <= strip_slots<P>() * slot_pitch<P>());
   const int nls = a.num_init + num_it * (a.U > kInlineUsers ? 2 : 1);
-  // the default (enabled == 1) takes the GZ schedules (MODE 0, 1: cfg2, cfg4, cfg4'); the
-  // staged-z kernel (cfg3, cfg5) measured slower than the three launches
-  if (fc.enabled == 1 && fused_mode<P>(a) == 2) return false;
+  // the default (enabled == 1) takes the GZ schedules (MODE 0, 1) with at least four stages
+  // (cfg4, cfg4'): the staged-z kernel (cfg3, cfg5) and the three-stage bench forward (cfg2)
+  // measured slower than the three launches on most boxes (DESIGN.md section 12,
+  // profiles/r04/ab_cfg2_fused_vs_three.txt)
+  if (fc.enabled == 1 && (fused_mode<P>(a) == 2 || a.num_init + num_it < 4)) return false;
   return items >= 2L * cus && a.U <= kFusedMaxUsers && a.num_init + num_it <= kFusedMaxStages &&
          nls <= kFusedMaxLS && 2 * a.A <= 32 && a.B <= kFusedMaxB && a.bits_max <= 16 && heads;
 }

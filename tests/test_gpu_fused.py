@@ -125,8 +125,8 @@ def test_fused_graph_replay():
     dev = "cuda:0"
     t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
     args = (t(case.y), t(case.pe), t(case.h_hat), t(case.active), t(case.mcs_mask))
-    eng.fused_config(enable=True)
-    if True:
+    eng.fused_config(enable="force")
+    try:
         st = torch.cuda.Stream()
         with torch.cuda.stream(st):
             eng.forward(*args, num_it=None, precision="f16")    # warm-up (workspace allocation)
@@ -137,6 +137,8 @@ def test_fused_graph_replay():
         for _ in range(3):
             g.replay()
         torch.cuda.synchronize()
+    finally:
+        eng.fused_config(enable=True)
     assert np.array_equal(ref["llr_raw"], llr.cpu().numpy())
     assert eng.fused_status(reset=True) == 0
 
@@ -154,16 +156,17 @@ def test_fused_error_reaches_caller():
     eng = engine_for(case)
     eng.check()                                   # clean before
     args = _device_args(case)
-    eng.fused_config(inject_err=4)
+    eng.fused_config(enable="force", inject_err=4)
     try:
         eng.forward(*args, num_it=None, precision="f16")
         with pytest.raises(NRXError) as ei:
             eng.check()
         assert ei.value.code == NRX_ERR_FUSED
+        eng.fused_config(enable="force", inject_err=0)
+        eng.forward(*args, num_it=None, precision="f16")
+        eng.check()                               # cleared by the failed check, clean again
     finally:
-        eng.fused_config(inject_err=0)
-    eng.forward(*args, num_it=None, precision="f16")
-    eng.check()                                   # cleared by the failed check, clean again
+        eng.fused_config(enable=True, inject_err=0)
 
 
 def test_fused_error_raised_by_sim_ber():
@@ -175,10 +178,11 @@ def test_fused_error_raised_by_sim_ber():
     from neural_rx_amd.receiver import CGNNEngine
     cfg = get_config("nrx_rt")
     eng = CGNNEngine(spec_from_config(cfg), W.load(cfg.label), 0)
+    eng.fused_config(enable="force")
     gen = SlotGenerator(GenParams.from_config(cfg, num_tx=2, num_prbs=4), device=0)
     ok = sim_ber(eng, gen, [8.0], batch_size=128, max_mc_iter=2, num_target_block_errors=10 ** 9, sync_every=2)
     assert ok.slots == 256
-    eng.fused_config(inject_err=2)
+    eng.fused_config(enable="force", inject_err=2)
     with pytest.raises(NRXError):
         sim_ber(eng, gen, [8.0], batch_size=128, max_mc_iter=2, num_target_block_errors=10 ** 9, sync_every=2)
     eng.close()
@@ -191,6 +195,7 @@ def test_fused_second_stream_refused_while_busy():
     from neural_rx_amd._lib import NRX_ERR_BUSY
     case = make_case("nrx_rt", batch=128, users=2, prbs=4, snr_db=12, seed=38)
     eng = engine_for(case)
+    eng.fused_config(enable="force")
     args = _device_args(case)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     with torch.cuda.stream(s1):
@@ -205,4 +210,5 @@ def test_fused_second_stream_refused_while_busy():
         eng.forward(*args, num_it=None, precision="f16")
     torch.cuda.synchronize()
     eng.check()
+    eng.fused_config(enable=True)
 

@@ -8,7 +8,8 @@ the dominant kernel (k_forward, else k_update averaged over its instantiations):
 
 * profiles/pmc_traffic.json[key]: ``k_forward_bytes_per_launch`` = 2 x FETCH_SIZE + WRITE_SIZE
   (KiB -> bytes; FETCH x 2 is the gfx950 correction of MI355X_MICROARCH.md's HBM section).
-* profiles/pmc_sq.json[key][kernel]: per-SIMD fractions of the wave lifetime --
+* profiles/pmc_sq.json[key][kernel] (k_forward, or k_update pooled over its instantiations for
+  the three-launch forward): per-SIMD fractions of the wave lifetime --
   ``mfma_busy_frac`` = SQ_VALU_MFMA_BUSY_CYCLES / SIMDs / lifetime, ``valu_issue_frac`` =
   SQ_INSTS_VALU x 4.5 cycles (the measured issue cost) / SIMDs /
   lifetime, ``wait_frac`` = SQ_WAIT_ANY / SQ_WAVE_CYCLES, where lifetime = 4 x SQ_WAVE_CYCLES /
@@ -57,6 +58,17 @@ def main(key, source, dirs, cus=256):
     pk = per_dispatch(dirs)
     fwd = {k: v for k, v in pk.items() if k.startswith("nrx::k_forward")}
     name, c = next(iter(fwd.items())) if fwd else (None, {})
+    sq_key = "k_forward"
+    if not fwd:
+        # three-launch forward: the dominant kernel is k_update (its instantiations pooled,
+        # per-dispatch means weighted by their dispatch counts)
+        cnt = dispatch_counts(dirs)
+        ups = {k: v for k, v in pk.items() if k.startswith("nrx::k_update")}
+        n = sum(cnt.get(k, 0) for k in ups)
+        if ups and n:
+            keys = set().union(*[set(v) for v in ups.values()])
+            c = {ck: sum(v.get(ck, 0.0) * cnt.get(k, 0) for k, v in ups.items()) / n for ck in keys}
+            name, sq_key = "nrx::k_update (all instantiations)", "k_update"
     traffic, sq = {}, {}
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         fb, wb = 2 * c["FETCH_SIZE"] * 1024, c["WRITE_SIZE"] * 1024
@@ -75,7 +87,7 @@ def main(key, source, dirs, cus=256):
         if "SQ_WAIT_ANY" in c:
             rec["wait_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
         rec["counters"] = {k: round(v, 1) for k, v in sorted(c.items())}
-        sq = {"k_forward": rec}
+        sq = {sq_key: rec}
     if not fwd:
         # three-launch forward (e.g. cfg5's per-GPU shard, U = 8): every kernel's bytes per
         # dispatch, and the forward's total = sum over kernels of mean x dispatches per forward
@@ -90,7 +102,10 @@ def main(key, source, dirs, cus=256):
                 kern[k] = {"bytes_per_dispatch": round(b), "dispatches_per_forward": per_fwd}
                 tot += b * per_fwd
         if kern:
+            ub = [(v["bytes_per_dispatch"], cnt.get(k, 0)) for k, v in kern.items() if k.startswith("nrx::k_update")]
+            nu = sum(n for _, n in ub)
             traffic = {"forward_bytes": round(tot), "kernels": kern, "source": source,
+                       "k_update_bytes_per_launch": round(sum(bb * n for bb, n in ub) / nu) if nu else None,
                        "unit": "bytes per forward (sum over its launches)",
                        "note": "2 x FETCH_SIZE + WRITE_SIZE per dispatch, rocprofv3 separate --pmc passes"}
     for fname, rec in (("pmc_traffic.json", traffic), ("pmc_sq.json", sq)):
@@ -102,7 +117,7 @@ def main(key, source, dirs, cus=256):
             data.setdefault(key, {}).update(rec)
         else:
             old = data.get(key, {})
-            if "k_update_bytes_per_launch" in old:
+            if "k_update_bytes_per_launch" in old and rec.get("k_update_bytes_per_launch") is None:
                 rec["k_update_bytes_per_launch"] = old["k_update_bytes_per_launch"]
                 rec.setdefault("earlier_source", {})["k_update_bytes_per_launch"] = old.get("source")
             data[key] = rec
