@@ -861,6 +861,7 @@ struct BlockParams {
   int inline_combine;                                    // U <= kInlineUsers: z-load forms a
   int norm_pre;                                          // a.norm[b] holds the slot norm (k_norm ran)
   int pair;                                              // k_update: two items per workgroup (2nd prefetched)
+  int gz;                                                // k_update: conv1 reads its z rows from memory
 };
 
 template <class P>
@@ -1687,7 +1688,7 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
     if constexpr (sizeof(S) == 2) {
       // one-launch forward: the pe16 rows of this item (every other user of the slot may skip too)
       const int lf = nrx_tid() / kTP, tt = nrx_tid() % kTP, f = f_start + lf;
-      if (fn && a.pe16 && lf >= kHalo && lf < kHalo + P::FO && lf < R0 && tt < kT && f >= 0 && f < F) {
+      if (a.pe16 && lf >= kHalo && lf < kHalo + P::FO && lf < R0 && tt < kT && f >= 0 && f < F) {
         const float2 pv = *reinterpret_cast<const float2*>(a.pe + (((size_t)u * F + f) * kT + tt) * 2);
         S pe2[8] = {};
         pe2[0] = (S)pv.x;
@@ -1771,7 +1772,7 @@ __device__ __forceinline__ void init_user(const BlockParams<P>& prm, char* smem,
     if constexpr (sizeof(S) == 2) {
       // one-launch forward: the pe16 chunk of this item's own rows for the update items' conv1
       // (every slot's StateInit items write the same bytes for a user's rows)
-      if (fn && a.pe16 && ok && lf >= kHalo && lf < kHalo + P::FO) {
+      if (a.pe16 && ok && lf >= kHalo && lf < kHalo + P::FO) {
         S pe2[8] = {};
         pe2[0] = (S)pv.x;
         pe2[1] = (S)pv.y;
@@ -2257,6 +2258,9 @@ __global__ __launch_bounds__(512) void k_init(BlockParams<P> prm) {
   stamp(5);
 }
 
+#ifndef NRX_UPDATE_GZ
+#define NRX_UPDATE_GZ 1
+#endif
 // UpdateState of one (slot, user, strip) with the fused tail.  grid = (strips, U, B).
 template <class P, int CHP, int TAILM>
 __global__ __launch_bounds__(512) void k_update(BlockParams<P> prm) {
@@ -2264,6 +2268,25 @@ __global__ __launch_bounds__(512) void k_update(BlockParams<P> prm) {
   int b, u, strip;
   work_item(blockIdx.x, prm.a.B, prm.a.U, prm.strips, prm.order_rev, b, u, strip);
   stamp(0);
+  if constexpr (std::is_same<P, P16>::value) {
+    if (prm.gz) {
+      // conv1 reads its z rows [a | s | pe] from L2 / HBM (GZ, as k_forward's update items): no
+      // z image, so neither the first item's chip-wide z load nor the paired item's DMA
+      constexpr int R0 = strip_slots<P>();
+      char* X = smem;
+      char* WB = smem + R0 * slot_pitch<P>();
+      zero_pad_symbols<P>(X);
+      gz_item_run<P, CHP, TAILM>(prm, X, WB, b, u, strip * P::FO - kHalo, nullptr, nullptr);
+      if (prm.pair) {
+        int b1, u1, s1;
+        work_item(blockIdx.x + gridDim.x, prm.a.B, prm.a.U, prm.strips, prm.order_rev, b1, u1, s1);
+        __syncthreads();   // every wave is past the first item's epilogue (WB, X)
+        gz_item_run<P, CHP, TAILM>(prm, X, WB, b1, u1, s1 * P::FO - kHalo, nullptr, nullptr);
+      }
+      stamp(5);
+      return;
+    }
+  }
   if constexpr ((TAILM == TAIL_AGG || TAILM == TAIL_READOUT_WB) && P::WLDS && NRX_PAIR != 0 && NRX_ZDMA != 0) {
     if (prm.pair) {
       int b1, u1, s1;
@@ -2688,6 +2711,9 @@ struct Launch {
     bp.a = args;
     bp.inline_combine = args.U <= kInlineUsers;
     bp.pair = 0;
+    bp.gz = 0;
+    if constexpr (std::is_same<P, P16>::value)   // 24-row strips, U <= 2, the workspace within GZ's offsets
+      bp.gz = NRX_UPDATE_GZ != 0 && args.U <= 2 && args.ws_bytes < kGzOob && args.pe16 != nullptr;
     bp.strips = strips;
     const int nq = args.F * kT * 2 * args.A / 4;
     bp.norm_pre = nq > kNormFusedMaxQ;
