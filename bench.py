@@ -296,6 +296,16 @@ def main():
             sq = json.load(open(sq_path)).get(key, {}).get("k_forward" if fused else "k_update", {})
         except Exception:
             sq = {}
+    # counters are quoted only from a capture of the library that is running:
+    # every record carries the nrx_build_id() of the library it profiled
+    from neural_rx_amd import _lib
+    build_id = _lib.load().nrx_build_id().decode()
+    tr_rec = pmc.get(key, {})
+    match = bool(sq) and sq.get("build_id") == build_id and (traffic is None and fwd_traffic is None
+                                                             or tr_rec.get("build_id") == build_id)
+    if not match:
+        traffic = fwd_traffic = pmc_src = None
+        sq = {k: v for k, v in sq.items() if k in ("source", "build_id")}
     whole_tflops = metrics.forward_flops_per_re_user(spec, num_it) * re_users * world / (elapsed / args.steps) / 1e12
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -327,7 +337,10 @@ def main():
                 "mixed_bound_tflops": round(mixed, 1) if mixed else None,
                 "frac_of_mixed_bound": round(achieved / mixed, 4) if mixed else None,
                 "mixed_bound_note": mixed_note,
-                "traffic_source": pmc_src}
+                "traffic_source": pmc_src,
+                "build_id": build_id,
+                "counters_build_id": sq.get("build_id"),
+                "counters_match_build": match}
     if fused:
         upd_items = args.steps * num_it * U * B * ((F + 23) // 24)
         roofline["fused_queue"] = {"update_items_waited": fused_st["waited"], "update_items": upd_items,

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NRX_API_VERSION 6
+#define NRX_API_VERSION 7
 
 enum nrx_status {
   NRX_OK = 0,
@@ -289,35 +289,47 @@ double nrx_flops_per_re_user(const nrx_desc* desc, int32_t num_it);
 int nrx_profile_enable(nrx_handle* h, int32_t enable);
 int nrx_profile_read(nrx_handle* h, int32_t kernel, int64_t* launches, double* total_ms);
 
-/* The throughput tier of nrx_forward (f16, 24-row strips, >= 2 items per CU, U <= 2, one
- * StateInit, one LLR head) runs the whole forward as ONE persistent launch whose items wait
- * on per-(stage, slot) counters in a handle-owned buffer.  status[3] since the last reset:
- * [0] error bits (1: a bounded dependency wait timed out, 2: items left undone -- the
- * results of that forward are invalid), [1] update items whose inputs were not complete when
- * the previous item polled for them (their z image loaded after a wait instead of during
- * that item's epilogue), [2] the polls those waits took.  Blocking: the stream of the last
- * forward is synchronised first; reset != 0 clears them.  Returns NRX_ERR_FUSED (message
- * with the bits) when the error word is non-zero, so a caller that only checks the status
- * code cannot miss it; status[] is filled either way.
+/* The one-launch forward (k_forward, f16 only): StateInit, every update and the readouts as ONE
+ * persistent launch whose items wait on per-(stage, slot) counters in a handle-owned buffer.
+ * It applies to f16 forwards with 24-row strips and at least two items per CU, U <= 8 users,
+ * 2A <= 32 (16 rx antennas), Var-IO (one StateInit stage per MCS), up to 8 iterations
+ * (num_init + num_it <= 12) and up to three LLR heads.  Which shapes take it by default is set
+ * by nrx_fused_config (default: the shapes where it measured faster -- U <= 2 with at least four
+ * stages, i.e. Var-IO and 8-iteration models such as BASELINE cfg4 / cfg4'; the 2-iteration
+ * bench forward, U > 2 and the large grids run the three-launch path).  status[3] since the
+ * last reset: [0] error bits (1: a bounded dependency wait timed out, 2: items left undone --
+ * the results of that forward are invalid), [1] update items whose inputs were not complete
+ * when the previous item polled for them, [2] the polls those waits took.  Blocking: waits for
+ * an event the handle recorded behind its last one-launch forward (not for the caller's stream,
+ * which may have been destroyed since); reset != 0 clears them.  Returns NRX_ERR_FUSED (message
+ * with the bits) when the error word is non-zero, so a caller that only checks the status code
+ * cannot miss it; status[] is filled either way.
  * Forwards on one handle must not run concurrently on several streams (the counters are per
- * handle): nrx_forward returns NRX_ERR_BUSY when a forward that would take this path arrives
- * on a stream other than the previous forward's while that stream still has work pending.
- * NRX_FUSED=0 in the environment (read by nrx_create) takes the three-launch path instead, 2
- * the one-launch forward wherever it applies. */
+ * handle): nrx_forward / nrx_forward_ex / nrx_forward_aerial return NRX_ERR_BUSY, before
+ * launching anything, when a forward that would take this path arrives on a stream other than
+ * the previous one-launch forward's while that forward has not finished.  Forwards captured
+ * into a hipGraph record no event: graph replays are outside this guard, so a caller replays
+ * one handle's graphs on one stream.  NRX_FUSED in the environment (read by nrx_create): 0/off
+ * the three-launch path, 1/on the default, 2/force wherever the path applies; any other value
+ * fails nrx_create with NRX_ERR_INVALID_ARG. */
 int nrx_fused_status(nrx_handle* h, int32_t* status, int32_t reset);
 
 /* Per-handle control of the one-launch forward: enable = 0 the three-launch path; 1 (default)
  * the one-launch forward for the shapes it is measured faster on (U <= 2 with conv1 reading its
  * rows from memory, at least four stages: Var-IO, 8 iterations); 2 for every shape it applies
  * to (also the 2-iteration bench forward, U <= 8 and 2A <= 32 with staged z images; outputs
- * identical to the three launches); < 0: unchanged.  The initial value comes from NRX_FUSED
- * (0 / 1 / 2) at nrx_create; spin_limit = dependency-wait polls before the timeout error (<= 0: the
- * default, ~0.5 s); inject_err = error bits the next forwards set in the error word (test
- * hook: callers must surface them; 0: none). */
+ * identical to the three launches).  The initial value comes from NRX_FUSED at nrx_create;
+ * spin_limit = dependency-wait polls before the timeout error (0: the default, ~0.5 s);
+ * inject_err = error bits the next forwards set in the error word (test hook: callers must
+ * surface them; 0: none).  Any argument < 0 leaves that setting unchanged. */
 int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t inject_err);
 
 const char* nrx_last_error(void);
 int32_t nrx_api_version(void);
+/* Content hash of the sources this library was built from (16 hex digits; set at link time by
+ * neural_rx_amd/build.py).  Recorded with every committed counter capture so that a bench line
+ * can tell whether the counters it quotes were taken from the library that is running. */
+const char* nrx_build_id(void);
 
 #ifdef __cplusplus
 }

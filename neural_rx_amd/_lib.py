@@ -28,6 +28,7 @@ EXPORTS = [
     "nrx_profile_enable", "nrx_profile_read", "nrx_aerial_workspace_size", "nrx_forward_aerial",
     "nrx_llr_demap", "nrx_gen_workspace_size", "nrx_generate_slots", "nrx_count_errors",
     "nrx_workspace_size_ex", "nrx_forward_ex", "nrx_fused_status", "nrx_fused_config",
+    "nrx_build_id",
 ]
 # enum nrx_y_layout
 Y_LAYOUTS = {"cgnn": 0, "sionna": 1, "split": 2}
@@ -238,6 +239,8 @@ def load(path: str = LIB_PATH):
     lib.nrx_count_errors.restype = c.c_int
     lib.nrx_api_version.argtypes = []
     lib.nrx_api_version.restype = c.c_int32
+    lib.nrx_build_id.argtypes = []
+    lib.nrx_build_id.restype = c.c_char_p
     _lib = lib
     return lib
 

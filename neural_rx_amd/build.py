@@ -7,6 +7,7 @@ travels to the GPU box with the repository snapshot).
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -14,10 +15,15 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "lib", "libnrx.so")
-SOURCES = [os.path.join(CSRC, "nrx_kernels.hip"), os.path.join(CSRC, "nrx_aerial.hip"),
-           os.path.join(CSRC, "nrx_synth.hip"), os.path.join(CSRC, "nrx_api.cpp")]
-DEPS = SOURCES + [os.path.join(CSRC, "nrx_internal.h"),
-                  os.path.join(HERE, "..", "include", "nrx.h")]
+# one translation unit per strip tier / k_forward mode, so that an edit of one schedule recompiles
+# only its own code object; nrx_device.inc / nrx_launch.inc hold the shared device and launch code
+KERNEL_TUS = ["nrx_k_p16.hip", "nrx_k_p16m.hip", "nrx_k_p16s.hip", "nrx_k_p64.hip", "nrx_k_fwd0.hip",
+              "nrx_k_fwd1.hip", "nrx_k_fwd2.hip", "nrx_dispatch.hip"]
+SOURCES = [os.path.join(CSRC, f) for f in KERNEL_TUS] + [
+    os.path.join(CSRC, "nrx_aerial.hip"), os.path.join(CSRC, "nrx_synth.hip"), os.path.join(CSRC, "nrx_api.cpp")]
+HEADERS = [os.path.join(CSRC, "nrx_internal.h"), os.path.join(HERE, "..", "include", "nrx.h")]
+KERNEL_INCS = [os.path.join(CSRC, "nrx_device.inc"), os.path.join(CSRC, "nrx_launch.inc")]
+DEPS = SOURCES + HEADERS + KERNEL_INCS
 ARCH = os.environ.get("NRX_OFFLOAD_ARCH", "gfx950")
 
 
@@ -37,14 +43,19 @@ def needs_build() -> bool:
     return any(_stale(os.path.join(OBJ_DIR, os.path.basename(s) + ".o"), s) for s in SOURCES)
 
 
-HEADERS = [os.path.join(CSRC, "nrx_internal.h"), os.path.join(HERE, "..", "include", "nrx.h")]
 OBJ_DIR = os.path.join(HERE, "lib", "obj")
+
+
+def _includes(src: str) -> list:
+    if os.path.basename(src) in KERNEL_TUS:
+        return HEADERS + KERNEL_INCS
+    return HEADERS
 
 
 def _sig(src: str) -> str:
     """mtimes of a source and the headers it includes, taken when its compile starts (an edit
     made while that compile runs leaves the object stale)"""
-    return " ".join(repr(os.path.getmtime(d)) for d in [src] + HEADERS if os.path.exists(d))
+    return " ".join(repr(os.path.getmtime(d)) for d in [src] + _includes(src) if os.path.exists(d))
 
 
 def _stale(obj: str, src: str) -> bool:
@@ -52,6 +63,30 @@ def _stale(obj: str, src: str) -> bool:
     if not os.path.exists(obj) or not os.path.exists(sig):
         return True
     return open(sig).read() != _sig(src)
+
+
+def source_hash() -> str:
+    """Content hash of every source the library is built from (the kernels, their includes, the
+    host side).  Compiled into the library (nrx_build_id) at every link, so a counter capture
+    (tools/pmc_record.py) and a later bench line can tell whether they describe the same kernels."""
+    h = hashlib.sha256()
+    for p in sorted(set(SOURCES + HEADERS + KERNEL_INCS)):
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _build_id_object(verbose: bool) -> str:
+    src = os.path.join(OBJ_DIR, "nrx_build_id.cpp")
+    obj = src + ".o"
+    with open(src, "w") as f:
+        f.write('extern "C" const char* nrx_build_id(void) { return "%s"; }\n' % source_hash())
+    cmd = [hipcc(), "-O2", "-fPIC", "-c", src, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return obj
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
@@ -87,6 +122,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
                 f.write(sig)
     if bad:
         raise subprocess.CalledProcessError(bad, "hipcc -c")
+    objs.append(_build_id_object(verbose))
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", *objs, "-o", tmp]
     if verbose:
         print(" ".join(cmd), flush=True)

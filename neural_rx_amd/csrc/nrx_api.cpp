@@ -24,7 +24,7 @@ hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args, co
                               int num_it, hipStream_t st, Prof* prof, const FusedCtl& fc);
 bool fused_would_run(const FwdArgs<_Float16, float, _Float16>& args, int num_it, const FusedCtl& fc);
 size_t fused_sync_bytes();
-hipError_t fused_sync_status(void* sync, int* st, bool reset, hipStream_t stream);
+hipError_t fused_sync_status(void* sync, int* st, bool reset, hipEvent_t last);
 hipError_t launch_forward_f64(const FwdArgs<double, double, float>& args,
                               const ModelW<double, double>& W, int num_it, hipStream_t st,
                               Prof* prof);
@@ -353,7 +353,13 @@ struct nrx_handle {
   int fused_enabled = 1;    // NRX_FUSED (environment, read once at nrx_create)
   int spin_limit = kFusedSpinLimit;
   int dbg_err = 0;
-  hipStream_t last_stream = nullptr;   // stream of the last one-launch forward
+  // one-stream rule of the one-launch forward: an event the handle owns, recorded
+  // behind every eager one-launch forward, stands for "that forward is done" -- the caller's
+  // stream itself is never kept (it may be destroyed between calls).  last_stream is compared,
+  // never used.  Forwards captured into a hipGraph record no event: graph replays are outside
+  // the guard (the caller keeps replays of one handle on one stream).
+  hipEvent_t last_ev = nullptr;
+  hipStream_t last_stream = nullptr;
   bool have_last = false;
   FusedCtl fused_ctl() const { return FusedCtl{fused_sync, fused_enabled, spin_limit, dbg_err}; }
 };
@@ -417,6 +423,21 @@ static void fill_args(FwdArgs<WT, BT, S>& a, const nrx_handle* h, const nrx_io* 
 }
 
 
+// NRX_ERR_BUSY when a forward that would take the one-launch path arrives on a stream other than
+// the previous one-launch forward's while that forward has not finished (the counters are per
+// handle).  Called before ANY launch of a forward entry point, so a refused call has launched
+// nothing (the y-layout / Aerial preprocessing used to run first).
+static int fused_busy(nrx_handle* h, const nrx_io* io, hipStream_t st, bool* takes) {
+  *takes = false;
+  if (io->precision != NRX_PREC_F16) return NRX_OK;
+  FwdArgs<_Float16, float, _Float16> a{};
+  fill_args(a, h, io, nullptr, h->m16.init_cinp);   // pointers unused: the decision needs sizes only
+  *takes = fused_would_run(a, io->num_it, h->fused_ctl());
+  if (*takes && h->have_last && h->last_stream != st && hipEventQuery(h->last_ev) == hipErrorNotReady)
+    return fail(NRX_ERR_BUSY, "a one-launch forward of this handle is still running on another stream");
+  return NRX_OK;
+}
+
 extern "C" {
 
 const char* nrx_last_error(void) { return g_err.c_str(); }
@@ -456,12 +477,22 @@ int nrx_create(const nrx_desc* desc, const float* const* weights, const int64_t*
   h->desc = *desc;
   h->device = device;
   {
-    const char* ev = getenv("NRX_FUSED");   // A/B and bit-identity tests: 0 = three launches
-    h->fused_enabled = ev ? atoi(ev) : 1;
-    if (h->fused_enabled < 0 || h->fused_enabled > 2) h->fused_enabled = 1;
+    // A/B and bit-identity tests: 0 = three launches, 1 = default, 2 (or "force") = wherever it
+    // applies; anything else is rejected rather than silently read as 0
+    const char* ev = getenv("NRX_FUSED");
+    if (ev && *ev) {
+      if (!strcmp(ev, "0") || !strcmp(ev, "off")) h->fused_enabled = 0;
+      else if (!strcmp(ev, "1") || !strcmp(ev, "on")) h->fused_enabled = 1;
+      else if (!strcmp(ev, "2") || !strcmp(ev, "force")) h->fused_enabled = 2;
+      else {
+        delete h;
+        return fail(NRX_ERR_INVALID_ARG, std::string("NRX_FUSED must be 0/off, 1/on or 2/force, got '") + ev + "'");
+      }
+    }
   }
   e = hipMalloc(&h->fused_sync, fused_sync_bytes());
   if (e == hipSuccess) e = hipMemset(h->fused_sync, 0, fused_sync_bytes());
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->last_ev, hipEventDisableTiming);
   if (e != hipSuccess) {
     nrx_destroy(h);
     return hip_fail(e, "fused forward counters");
@@ -481,6 +512,7 @@ void nrx_destroy(nrx_handle* h) {
   if (h->m16.dev) (void)hipFree(h->m16.dev);
   if (h->m64.dev) (void)hipFree(h->m64.dev);
   if (h->fused_sync) (void)hipFree(h->fused_sync);
+  if (h->last_ev) (void)hipEventDestroy(h->last_ev);
   delete h->prof;
   delete h;
 }
@@ -515,18 +547,18 @@ int nrx_forward(nrx_handle* h, const nrx_io* io, void* workspace, size_t workspa
     FwdArgs<_Float16, float, _Float16> a{};
     fill_args(a, h, io, workspace, h->m16.init_cinp);
     const FusedCtl fc = h->fused_ctl();
-    if (fused_would_run(a, io->num_it, fc)) {
-      // one stream per handle on this path (the counters are per handle): a forward on another
-      // stream is refused while the previous one's stream still has work
-      if (h->have_last && h->last_stream != st) {
-        const hipError_t q = hipStreamQuery(h->last_stream);
-        if (q == hipErrorNotReady)
-          return fail(NRX_ERR_BUSY, "a one-launch forward of this handle is still running on another stream");
-      }
-      h->last_stream = st;
-      h->have_last = true;
-    }
+    const bool takes = fused_would_run(a, io->num_it, fc);
+    if (takes && h->have_last && h->last_stream != st && hipEventQuery(h->last_ev) == hipErrorNotReady)
+      return fail(NRX_ERR_BUSY, "a one-launch forward of this handle is still running on another stream");
     e = launch_forward_f16(a, h->m16.W, io->num_it, st, h->prof, fc);
+    if (e == hipSuccess && takes) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+        e = hipEventRecord(h->last_ev, st);
+        h->last_stream = st;
+        h->have_last = e == hipSuccess;
+      }
+    }
   } else {
     FwdArgs<double, double, float> a{};
     fill_args(a, h, io, workspace, h->m64.init_cinp);
@@ -563,6 +595,8 @@ int nrx_forward_ex(nrx_handle* h, const nrx_io* io, int32_t y_layout, const floa
     return fail(NRX_ERR_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes");
   if (!io->y || ((y_layout == NRX_Y_SPLIT) != (y_imag != nullptr)))
     return fail(NRX_ERR_INVALID_ARG, "y / y_imag do not match the y layout");
+  bool takes = false;
+  if ((rc = fused_busy(h, io, (hipStream_t)stream, &takes))) return rc;
   const size_t yb = y_cgnn_bytes(h, &io->shape);
   float* ycg = (float*)workspace;
   hipError_t e = launch_y_layout(io->y, y_imag, y_layout, io->shape.batch, io->shape.num_subcarriers,
@@ -648,6 +682,14 @@ int nrx_forward_aerial(nrx_handle* h, const nrx_aerial_io* io, void* workspace, 
   const nrx_shape& s = io->shape;
   const int A = h->desc.num_rx_ant;
   hipStream_t st = (hipStream_t)stream;
+  {
+    nrx_io q{};
+    q.shape = s;
+    q.num_it = io->num_it;
+    q.precision = io->precision;
+    bool takes = false;
+    if ((rc = fused_busy(h, &q, st, &takes))) return rc;
+  }
   hipError_t e = launch_aerial_tables(io->dmrs_ofdm_pos, io->dmrs_subcarrier_pos, s.num_tx, io->num_dmrs_symbols,
                                       io->num_dmrs_subcarriers, s.num_symbols, s.num_subcarriers, w.nn, w.pe, st);
   if (e == hipSuccess)
@@ -779,7 +821,7 @@ int nrx_profile_enable(nrx_handle* h, int32_t enable) {
 int nrx_fused_status(nrx_handle* h, int32_t* status, int32_t reset) {
   if (!h || !status) return fail(NRX_ERR_INVALID_ARG, "null argument");
   int st[3] = {0, 0, 0};
-  hipError_t e = fused_sync_status(h->fused_sync, st, reset != 0, h->have_last ? h->last_stream : nullptr);
+  hipError_t e = fused_sync_status(h->fused_sync, st, reset != 0, h->have_last ? h->last_ev : nullptr);
   if (e != hipSuccess) return hip_fail(e, "fused status");
   for (int i = 0; i < 3; ++i) status[i] = st[i];
   if (st[0])
@@ -790,9 +832,11 @@ int nrx_fused_status(nrx_handle* h, int32_t* status, int32_t reset) {
 
 int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t inject_err) {
   if (!h) return fail(NRX_ERR_INVALID_ARG, "null argument");
+  // every argument < 0 leaves its setting unchanged; spin_limit == 0 restores the
+  // default bound
   if (enable >= 0) h->fused_enabled = enable > 2 ? 2 : enable;
-  h->spin_limit = spin_limit > 0 ? spin_limit : kFusedSpinLimit;
-  h->dbg_err = inject_err;
+  if (spin_limit >= 0) h->spin_limit = spin_limit > 0 ? spin_limit : kFusedSpinLimit;
+  if (inject_err >= 0) h->dbg_err = inject_err;
   return NRX_OK;
 }
 

@@ -111,13 +111,22 @@ class CGNNEngine:
         st = (ctypes.c_int32 * 3)()
         _lib.check(self._lib.nrx_fused_status(self._h, st, 1))
 
-    def fused_config(self, enable=None, spin_limit: int = 0, inject_err: int = 0):
-        """One-launch forward control (include/nrx.h nrx_fused_config): ``enable`` False / True
-        (where it is the faster schedule) / "force" (every shape it applies to), None:
-        unchanged; the dependency-wait bound (<= 0: default) and error bits to inject (test
-        hook)."""
-        en = -1 if enable is None else (2 if enable == "force" else int(bool(enable)))
-        _lib.check(self._lib.nrx_fused_config(self._h, en, int(spin_limit), int(inject_err)))
+    def fused_config(self, enable=None, spin_limit: Optional[int] = None, inject_err: Optional[int] = None):
+        """One-launch forward control (include/nrx.h nrx_fused_config): ``enable`` False / 0,
+        True / 1 (where it is the faster schedule), "force" / 2 (every shape it applies to), None:
+        unchanged; the dependency-wait bound (0: default) and error bits to inject (test hook),
+        None: unchanged."""
+        if enable is None:
+            en = -1
+        elif enable == "force" or (isinstance(enable, int) and not isinstance(enable, bool) and enable == 2):
+            en = 2
+        elif isinstance(enable, (bool, int)) and int(enable) in (0, 1):
+            en = int(enable)
+        else:
+            raise ValueError(f"enable must be False/0, True/1, 'force'/2 or None, got {enable!r}")
+        sl = -1 if spin_limit is None else max(int(spin_limit), 0)
+        ie = -1 if inject_err is None else int(inject_err)
+        _lib.check(self._lib.nrx_fused_config(self._h, en, sl, ie))
 
     def profile_read(self):
         """{kernel: (launches, total_ms)} since the last profile(True)."""

@@ -32,7 +32,7 @@ def test_exports_every_header_symbol(lib):
     assert set(syms) == set(_lib.EXPORTS)
     for s in syms:
         assert hasattr(lib, s), s
-    assert lib.nrx_api_version() == 6
+    assert lib.nrx_api_version() == 7
 
 
 @pytest.mark.parametrize("name", sorted(BUILTIN))

@@ -199,8 +199,8 @@ def test_fused_second_stream_refused_while_busy():
     args = _device_args(case)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     with torch.cuda.stream(s1):
+        torch.cuda._sleep(50_000_000)             # the forward queued behind a spin kernel
         eng.forward(*args, num_it=None, precision="f16")
-        torch.cuda._sleep(50_000_000)             # keep s1 busy (spin kernel)
     with torch.cuda.stream(s2):
         with pytest.raises(NRXError) as ei:
             eng.forward(*args, num_it=None, precision="f16")
@@ -212,3 +212,34 @@ def test_fused_second_stream_refused_while_busy():
     eng.check()
     eng.fused_config(enable=True)
 
+
+
+def test_fused_guard_survives_destroyed_stream():
+    """The one-stream guard keeps an event of its own, not the caller's stream: after
+    the first forward's stream is destroyed, a forward on a second stream runs and check()
+    waits on that event, not on the dead stream handle."""
+    import ctypes
+    import torch
+    case = make_case("nrx_rt", batch=128, users=2, prbs=4, snr_db=12, seed=39)
+    eng = engine_for(case)
+    eng.fused_config(enable="force")
+    args = _device_args(case)
+    # the HIP runtime torch loaded (by its path: a second runtime in the process sees no GPUs)
+    path = next(l.split()[-1] for l in open("/proc/self/maps").read().splitlines() if "libamdhip64" in l)
+    hip = ctypes.CDLL(path)
+    raw = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(raw)) == 0
+    try:
+        s1 = torch.cuda.ExternalStream(raw.value)
+        with torch.cuda.stream(s1):
+            eng.forward(*args, num_it=None, precision="f16")
+        s1.synchronize()
+        del s1
+        assert hip.hipStreamDestroy(raw) == 0    # the handle's last forward stream is gone
+        s2 = torch.cuda.Stream()
+        with torch.cuda.stream(s2):
+            eng.forward(*args, num_it=None, precision="f16")
+        eng.check()
+        s2.synchronize()
+    finally:
+        eng.fused_config(enable=True)

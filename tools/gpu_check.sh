@@ -1,5 +1,5 @@
-# Round-4 check of the tree: GPU tests, smoke, default bench line (+ optional kernel trace).
-# usage (GPU box): bash tools/gpu_r04_check.sh <tag> [kt|-] [notests]
+#  check of the tree: GPU tests, smoke, default bench line (+ optional kernel trace).
+# usage (GPU box): bash tools/gpu_check.sh <tag> [kt|-] [notests]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/$1; mkdir -p $O

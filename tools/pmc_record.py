@@ -14,6 +14,8 @@ the dominant kernel (k_forward, else k_update averaged over its instantiations):
   SQ_INSTS_VALU x 4.5 cycles (the measured issue cost) / SIMDs /
   lifetime, ``wait_frac`` = SQ_WAIT_ANY / SQ_WAVE_CYCLES, where lifetime = 4 x SQ_WAVE_CYCLES /
   SQ_WAVES (SQ_WAVE_CYCLES counts quad-cycles) and SIMDs = 4 x CUs.
+Every record carries ``build_id`` = nrx_build_id() of the profiled library; bench.py quotes the
+counters only when it matches the library it runs (``roofline.counters_match_build``).
 """
 import collections
 import csv
@@ -54,7 +56,15 @@ def dispatch_counts(dirs):
     return {}
 
 
+def running_build_id():
+    """nrx_build_id() of the in-tree libnrx.so -- the library the passes just profiled"""
+    sys.path.insert(0, ROOT)
+    from neural_rx_amd import _lib
+    return _lib.load().nrx_build_id().decode()
+
+
 def main(key, source, dirs, cus=256):
+    build_id = running_build_id()
     pk = per_dispatch(dirs)
     fwd = {k: v for k, v in pk.items() if k.startswith("nrx::k_forward")}
     name, c = next(iter(fwd.items())) if fwd else (None, {})
@@ -72,14 +82,14 @@ def main(key, source, dirs, cus=256):
     traffic, sq = {}, {}
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         fb, wb = 2 * c["FETCH_SIZE"] * 1024, c["WRITE_SIZE"] * 1024
-        traffic = {"k_forward_bytes_per_launch": round(fb + wb), "source": source,
+        traffic = {"k_forward_bytes_per_launch": round(fb + wb), "source": source, "build_id": build_id,
                    "kernels": {name: {"fetch_bytes_corrected": fb, "write_bytes": wb, "bytes": fb + wb}},
                    "unit": "bytes per launch",
                    "note": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), rocprofv3 separate --pmc passes"}
     if "SQ_WAVE_CYCLES" in c and "SQ_WAVES" in c:
         simds = 4 * cus
         life = 4 * c["SQ_WAVE_CYCLES"] / c["SQ_WAVES"]
-        rec = {"kernel": name, "source": source, "wave_lifetime_cycles": round(life)}
+        rec = {"kernel": name, "source": source, "wave_lifetime_cycles": round(life), "build_id": build_id}
         if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
             rec["mfma_busy_frac"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / simds / life, 4)
         if "SQ_INSTS_VALU" in c:
@@ -104,7 +114,7 @@ def main(key, source, dirs, cus=256):
         if kern:
             ub = [(v["bytes_per_dispatch"], cnt.get(k, 0)) for k, v in kern.items() if k.startswith("nrx::k_update")]
             nu = sum(n for _, n in ub)
-            traffic = {"forward_bytes": round(tot), "kernels": kern, "source": source,
+            traffic = {"forward_bytes": round(tot), "kernels": kern, "source": source, "build_id": build_id,
                        "k_update_bytes_per_launch": round(sum(bb * n for bb, n in ub) / nu) if nu else None,
                        "unit": "bytes per forward (sum over its launches)",
                        "note": "2 x FETCH_SIZE + WRITE_SIZE per dispatch, rocprofv3 separate --pmc passes"}
