@@ -251,7 +251,7 @@ def main():
     fused = prof.get("forward", (0, 0.0))[0] > 0
     # the dominant kernel: the one-launch forward when the engine took it (throughput tier),
     # else the state-update launch of the three-launch forward
-    dom = "forward" if fused else "state_update"
+    dom = "forward" if fused else ("state_update_rr" if prof.get("state_update_rr", (0, 0.0))[0] else "state_update")
     dom_avg_s = prof[dom][1] / prof[dom][0] * 1e-3 * scale
     dom_flops = kflops[dom] * re_users
     peak = metrics.PEAK_TFLOPS[args.precision]
@@ -270,7 +270,9 @@ def main():
                       "f16 MFMA peak, pipes overlapped (metrics.forward_mixed_bound_tflops)")
     else:
         alg_bytes = metrics.update_launch_bytes_per_re_user(spec, num_it, elem) * re_users
-        pmc_field, kname = "k_update_bytes_per_launch", "k_update (3 sep-convs + fused aggregation/readout tail)"
+        pmc_field, kname = "k_update_bytes_per_launch", (
+            "k_update_rr (register-resident update launch: 3 sep-convs + fused aggregation/readout tail)"
+            if dom == "state_update_rr" else "k_update (3 sep-convs + fused aggregation/readout tail)")
         mixed = metrics.mixed_bound_tflops(spec, num_it, peak) if args.precision == "f16" else None
         mixed_note = ("k_update's depthwise FLOPs at the VALU peak (157 TF) + its dense FLOPs at the f16 "
                       "MFMA peak, pipes overlapped (metrics.mixed_bound_tflops)")

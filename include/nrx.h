@@ -283,7 +283,8 @@ double nrx_flops_per_re_user(const nrx_desc* desc, int32_t num_it);
  * every kernel launch on the launch stream (not graph-capture safe).  Kernel ids:
  * 0 norm, 1 state-init (+ fused aggregation tail), 2 state-update (+ fused aggregation
  * or readout tail), 3 the one-launch forward (StateInit + updates + readouts; see
- * nrx_fused_status for when it is taken).
+ * nrx_fused_status for when it is taken), 4 the register-resident state-update launch
+ * (nrx_update_schedule).
  * nrx_profile_enable(h, 1) (re)starts the counters; nrx_profile_read waits for the
  * recorded events and returns the launch count and summed device time of a kernel. */
 int nrx_profile_enable(nrx_handle* h, int32_t enable);
@@ -323,6 +324,14 @@ int nrx_fused_status(nrx_handle* h, int32_t* status, int32_t reset);
  * inject_err = error bits the next forwards set in the error word (test hook: callers must
  * surface them; 0: none).  Any argument < 0 leaves that setting unchanged. */
 int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t inject_err);
+
+/* Update-stage schedule of the three-launch f16 forward: update_rr = 1 (default) runs the
+ * register-resident update launch (layer outputs kept in registers, weights staged once per
+ * workgroup, 16-subcarrier strips) wherever it applies -- U <= 2 with conv1 reading its rows
+ * from memory, 2A <= 32, one LLR head whose readout fits -- and the strip update kernels
+ * elsewhere; 0 the strip kernels everywhere; < 0 unchanged.  Outputs are bit-identical either
+ * way.  The initial value comes from NRX_UPDATE_RR (0 / 1) at nrx_create. */
+int nrx_update_schedule(nrx_handle* h, int32_t update_rr);
 
 const char* nrx_last_error(void);
 int32_t nrx_api_version(void);

@@ -28,11 +28,11 @@ EXPORTS = [
     "nrx_profile_enable", "nrx_profile_read", "nrx_aerial_workspace_size", "nrx_forward_aerial",
     "nrx_llr_demap", "nrx_gen_workspace_size", "nrx_generate_slots", "nrx_count_errors",
     "nrx_workspace_size_ex", "nrx_forward_ex", "nrx_fused_status", "nrx_fused_config",
-    "nrx_build_id",
+    "nrx_build_id", "nrx_update_schedule",
 ]
 # enum nrx_y_layout
 Y_LAYOUTS = {"cgnn": 0, "sionna": 1, "split": 2}
-KERNELS = ["norm", "state_init", "state_update", "forward"]
+KERNELS = ["norm", "state_init", "state_update", "forward", "state_update_rr"]
 
 
 class NRXLibraryError(RuntimeError):
@@ -239,6 +239,8 @@ def load(path: str = LIB_PATH):
     lib.nrx_count_errors.restype = c.c_int
     lib.nrx_api_version.argtypes = []
     lib.nrx_api_version.restype = c.c_int32
+    lib.nrx_update_schedule.argtypes = [c.c_void_p, c.c_int32]
+    lib.nrx_update_schedule.restype = c.c_int
     lib.nrx_build_id.argtypes = []
     lib.nrx_build_id.restype = c.c_char_p
     _lib = lib

@@ -18,11 +18,12 @@ LIB = os.path.join(HERE, "lib", "libnrx.so")
 # one translation unit per strip tier / k_forward mode, so that an edit of one schedule recompiles
 # only its own code object; nrx_device.inc / nrx_launch.inc hold the shared device and launch code
 KERNEL_TUS = ["nrx_k_p16.hip", "nrx_k_p16m.hip", "nrx_k_p16s.hip", "nrx_k_p64.hip", "nrx_k_fwd0.hip",
-              "nrx_k_fwd1.hip", "nrx_k_fwd2.hip", "nrx_dispatch.hip"]
+              "nrx_k_fwd1.hip", "nrx_k_fwd2.hip", "nrx_k_rr.hip", "nrx_dispatch.hip"]
 SOURCES = [os.path.join(CSRC, f) for f in KERNEL_TUS] + [
     os.path.join(CSRC, "nrx_aerial.hip"), os.path.join(CSRC, "nrx_synth.hip"), os.path.join(CSRC, "nrx_api.cpp")]
 HEADERS = [os.path.join(CSRC, "nrx_internal.h"), os.path.join(HERE, "..", "include", "nrx.h")]
-KERNEL_INCS = [os.path.join(CSRC, "nrx_device.inc"), os.path.join(CSRC, "nrx_launch.inc")]
+KERNEL_INCS = [os.path.join(CSRC, "nrx_device.inc"), os.path.join(CSRC, "nrx_launch.inc"),
+               os.path.join(CSRC, "nrx_rr.inc")]
 DEPS = SOURCES + HEADERS + KERNEL_INCS
 ARCH = os.environ.get("NRX_OFFLOAD_ARCH", "gfx950")
 
@@ -77,11 +78,11 @@ def source_hash() -> str:
     return h.hexdigest()[:16]
 
 
-def _build_id_object(verbose: bool) -> str:
-    src = os.path.join(OBJ_DIR, "nrx_build_id.cpp")
+def _build_id_object(verbose: bool, obj_dir: str = OBJ_DIR, tag: str = "") -> str:
+    src = os.path.join(obj_dir, "nrx_build_id.cpp")
     obj = src + ".o"
     with open(src, "w") as f:
-        f.write('extern "C" const char* nrx_build_id(void) { return "%s"; }\n' % source_hash())
+        f.write('extern "C" const char* nrx_build_id(void) { return "%s%s"; }\n' % (source_hash(), tag))
     cmd = [hipcc(), "-O2", "-fPIC", "-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -89,18 +90,20 @@ def _build_id_object(verbose: bool) -> str:
     return obj
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
+def build(force: bool = False, verbose: bool = True, lib: str = LIB, obj_dir: str = OBJ_DIR,
+          extra_flags=()) -> str:
     """Compile the sources whose object is stale (force: all of them), in parallel, then link.
     Objects are kept in lib/obj/ (git-ignored) so that an edit of one source recompiles only
-    that source."""
-    if not force and not needs_build():
+    that source.  lib / obj_dir / extra_flags: a diagnostic variant library (tools/build_variants.py)."""
+    if lib == LIB and not force and not needs_build():
         return LIB
-    os.makedirs(OBJ_DIR, exist_ok=True)
-    tmp = LIB + f".tmp{os.getpid()}"
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+    os.makedirs(obj_dir, exist_ok=True)
+    tmp = lib + f".tmp{os.getpid()}"
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+             *extra_flags]
     objs, procs = [], []
     for src in SOURCES:
-        obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
         objs.append(obj)
         if not force and not _stale(obj, src):
             continue
@@ -122,13 +125,14 @@ def build(force: bool = False, verbose: bool = True) -> str:
                 f.write(sig)
     if bad:
         raise subprocess.CalledProcessError(bad, "hipcc -c")
-    objs.append(_build_id_object(verbose))
+    # a variant library carries its flags in the id, so its counters never pass for the default's
+    objs.append(_build_id_object(verbose, obj_dir, "+" + "".join(extra_flags) if extra_flags else ""))
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", *objs, "-o", tmp]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":

@@ -353,6 +353,7 @@ struct nrx_handle {
   int fused_enabled = 1;    // NRX_FUSED (environment, read once at nrx_create)
   int spin_limit = kFusedSpinLimit;
   int dbg_err = 0;
+  int update_rr = 1;        // nrx_update_schedule (NRX_UPDATE_RR at nrx_create)
   // one-stream rule of the one-launch forward: an event the handle owns, recorded
   // behind every eager one-launch forward, stands for "that forward is done" -- the caller's
   // stream itself is never kept (it may be destroyed between calls).  last_stream is compared,
@@ -361,7 +362,7 @@ struct nrx_handle {
   hipEvent_t last_ev = nullptr;
   hipStream_t last_stream = nullptr;
   bool have_last = false;
-  FusedCtl fused_ctl() const { return FusedCtl{fused_sync, fused_enabled, spin_limit, dbg_err}; }
+  FusedCtl fused_ctl() const { return FusedCtl{fused_sync, fused_enabled, spin_limit, dbg_err, update_rr}; }
 };
 
 static size_t state_bytes(const nrx_shape* s, int precision) {
@@ -388,6 +389,7 @@ static void fill_args(FwdArgs<WT, BT, S>& a, const nrx_handle* h, const nrx_io* 
   const nrx_desc* d = &h->desc;
   const nrx_shape* s = &io->shape;
   a.B = s->batch;
+  a.llr_B = s->batch;
   a.U = s->num_tx;
   a.F = s->num_subcarriers;
   a.A = d->num_rx_ant;
@@ -422,6 +424,8 @@ static void fill_args(FwdArgs<WT, BT, S>& a, const nrx_handle* h, const nrx_io* 
   a.ws_bytes = total < 0xFFFFFFFFull ? (unsigned)total : 0xFFFFFFFFu;
 }
 
+
+static int forward_slots(nrx_handle* h, const nrx_io* io, int llr_B, void* workspace, hipStream_t st);
 
 // NRX_ERR_BUSY when a forward that would take the one-launch path arrives on a stream other than
 // the previous one-launch forward's while that forward has not finished (the counters are per
@@ -490,6 +494,17 @@ int nrx_create(const nrx_desc* desc, const float* const* weights, const int64_t*
       }
     }
   }
+  {
+    const char* ev = getenv("NRX_UPDATE_RR");   // A/B: 0 = strip update kernels
+    if (ev && *ev) {
+      if (!strcmp(ev, "0")) h->update_rr = 0;
+      else if (!strcmp(ev, "1")) h->update_rr = 1;
+      else {
+        delete h;
+        return fail(NRX_ERR_INVALID_ARG, std::string("NRX_UPDATE_RR must be 0 or 1, got '") + ev + "'");
+      }
+    }
+  }
   e = hipMalloc(&h->fused_sync, fused_sync_bytes());
   if (e == hipSuccess) e = hipMemset(h->fused_sync, 0, fused_sync_bytes());
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->last_ev, hipEventDisableTiming);
@@ -517,14 +532,36 @@ void nrx_destroy(nrx_handle* h) {
   delete h;
 }
 
+static size_t ws_bytes_of(const nrx_shape* s, int precision) {
+  return align256((size_t)s->batch * sizeof(double)) + 4 * state_bytes(s, precision) + pe16_bytes(s, precision);
+}
+
+// Slots per sub-forward.  An f16 forward whose workspace would reach kGzRange runs as
+// consecutive forwards of at most this many slots on the caller's stream (slots are independent,
+// neural_rx.py:544-595 has no cross-slot term), each in the same workspace: conv1's z-row loader
+// then always addresses it with 32-bit buffer offsets, and the workspace shrinks to one chunk's.
+static int chunk_slots(const nrx_shape* s, int precision) {
+  if (precision != NRX_PREC_F16 || ws_bytes_of(s, precision) < kGzRange) return s->batch;
+  int lo = 1, hi = s->batch - 1;   // the largest chunk below the range (one slot always fits: F <= 3300)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) / 2;
+    nrx_shape c = *s;
+    c.batch = mid;
+    if (ws_bytes_of(&c, precision) < kGzRange) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
 int nrx_workspace_size(const nrx_handle* h, const nrx_shape* shape, int32_t precision, size_t* bytes) {
   if (!h || !bytes) return fail(NRX_ERR_INVALID_ARG, "null argument");
   int rc = check_shape(shape);
   if (rc) return rc;
   if (precision != NRX_PREC_F16 && precision != NRX_PREC_F32X)
     return fail(NRX_ERR_INVALID_ARG, "unknown precision");
-  *bytes = align256((size_t)shape->batch * sizeof(double)) + 4 * state_bytes(shape, precision) +
-           pe16_bytes(shape, precision);
+  nrx_shape c = *shape;
+  c.batch = chunk_slots(shape, precision);
+  *bytes = ws_bytes_of(&c, precision);
   return NRX_OK;
 }
 
@@ -542,10 +579,36 @@ int nrx_forward(nrx_handle* h, const nrx_io* io, void* workspace, size_t workspa
   if (!workspace || workspace_bytes < need)
     return fail(NRX_ERR_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes");
   hipStream_t st = (hipStream_t)stream;
+  const int bc = chunk_slots(&io->shape, io->precision);
+  if (bc < io->shape.batch) {
+    // slot chunks (chunk_slots): the same forward on [b0, b0 + n) with offset tensors; the LLR
+    // tensor keeps its head stride (llr_B)
+    const int B = io->shape.batch, U = io->shape.num_tx, F = io->shape.num_subcarriers, A2 = 2 * d->num_rx_ant;
+    const size_t re = (size_t)F * kT;
+    for (int b0 = 0; b0 < B; b0 += bc) {
+      nrx_io c = *io;
+      c.shape.batch = b0 + bc < B ? bc : B - b0;
+      c.y = io->y + (size_t)b0 * re * A2;
+      c.h_hat = io->h_hat ? io->h_hat + (size_t)b0 * U * re * A2 : nullptr;
+      c.active = io->active + (size_t)b0 * U;
+      c.mcs_mask = io->mcs_mask ? io->mcs_mask + (size_t)b0 * U * d->num_mcs : nullptr;
+      c.h_ref = io->h_ref ? io->h_ref + (size_t)b0 * U * re * A2 : nullptr;
+      c.llr = io->llr + (size_t)b0 * U * re * bits_max(d);
+      rc = forward_slots(h, &c, B, workspace, st);
+      if (rc) return rc;
+    }
+    return NRX_OK;
+  }
+  return forward_slots(h, io, io->shape.batch, workspace, st);
+}
+
+// One forward over io->shape.batch slots of an LLR tensor of llr_B slots (its head stride).
+static int forward_slots(nrx_handle* h, const nrx_io* io, int llr_B, void* workspace, hipStream_t st) {
   hipError_t e;
   if (io->precision == NRX_PREC_F16) {
     FwdArgs<_Float16, float, _Float16> a{};
     fill_args(a, h, io, workspace, h->m16.init_cinp);
+    a.llr_B = llr_B;
     const FusedCtl fc = h->fused_ctl();
     const bool takes = fused_would_run(a, io->num_it, fc);
     if (takes && h->have_last && h->last_stream != st && hipEventQuery(h->last_ev) == hipErrorNotReady)
@@ -562,6 +625,7 @@ int nrx_forward(nrx_handle* h, const nrx_io* io, void* workspace, size_t workspa
   } else {
     FwdArgs<double, double, float> a{};
     fill_args(a, h, io, workspace, h->m64.init_cinp);
+    a.llr_B = llr_B;
     e = launch_forward_f64(a, h->m64.W, io->num_it, st, h->prof);
   }
   if (e != hipSuccess) return hip_fail(e, "kernel launch");
@@ -837,6 +901,12 @@ int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t 
   if (enable >= 0) h->fused_enabled = enable > 2 ? 2 : enable;
   if (spin_limit >= 0) h->spin_limit = spin_limit > 0 ? spin_limit : kFusedSpinLimit;
   if (inject_err >= 0) h->dbg_err = inject_err;
+  return NRX_OK;
+}
+
+int nrx_update_schedule(nrx_handle* h, int32_t update_rr) {
+  if (!h) return fail(NRX_ERR_INVALID_ARG, "null argument");
+  if (update_rr >= 0) h->update_rr = update_rr ? 1 : 0;
   return NRX_OK;
 }
 

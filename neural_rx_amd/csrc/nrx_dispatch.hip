@@ -14,7 +14,7 @@ hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args,
     if (small_strips_fit<P16M>(args)) return run_tier_p16m(args, W, num_it, st, prof);
   }
   if (fused_applicable<P16>(args, num_it, fc)) return run_fused<P16>(args, W, num_it, st, prof, fc);
-  return run_tier_p16(args, W, num_it, st, prof);
+  return run_tier_p16(args, W, num_it, st, prof, fc.update_rr);
 }
 
 bool fused_would_run(const FwdArgs<_Float16, float, _Float16>& args, int num_it, const FusedCtl& fc) {
@@ -47,7 +47,7 @@ hipError_t setup_kernels() {
   (void)cu_count();
   (void)xcc_count();
   const hipError_t es[] = {setup_tier_p16(),     setup_tier_p16m(),    setup_tier_p16s(),   setup_tier_p64(),
-                           setup_kforward_m0(), setup_kforward_m1(), setup_kforward_m2()};
+                           setup_kforward_m0(), setup_kforward_m1(), setup_kforward_m2(), setup_update_rr()};
   for (hipError_t e : es)
     if (e != hipSuccess) return e;
   return hipSuccess;

@@ -29,6 +29,10 @@ constexpr int kInlineUsers = 4;  // users whose leave-one-out combine the update
 constexpr int kMaxHeads = 8;
 constexpr int kMaxUsers = 16;
 constexpr int kHalo = 3;      // 3 stacked 3x3 convs per block
+// f16 workspaces stay below this many bytes: conv1's z-row loader (struct GZ) addresses the
+// workspace through one buffer descriptor with 32-bit offsets and marks zero chunks with offsets
+// at or beyond it; a larger forward runs in slot chunks (nrx_api.cpp chunk_slots)
+constexpr unsigned kGzRange = 0x40000000u;
 
 // ---- LDS images of the f16 weights (kernels: SepStage / DenseStage).  A W^T [COUTP][CINP] image is a stack
 // of 16-row tiles addressed like an activation image: element (co, chunk q of 8 inputs) at
@@ -80,6 +84,8 @@ struct ModelW {
 template <class WT, class BT, class S>
 struct FwdArgs {
   int B, U, F, A, M, H;            // H = number of LLR heads
+  int llr_B;                       // slots of the caller's llr tensor (the head stride; > B when
+                                   // the forward runs in slot chunks, nrx_api.cpp)
   int init_cinp;                   // padded StateInit input width
   int num_init;
   int masking;
@@ -114,12 +120,13 @@ struct FusedCtl {
   int enabled;   // 0 off, 1 where measured faster (the bench-type schedule), 2 every applicable shape
   int spin_limit;
   int dbg_err;
+  int update_rr;   // three-launch f16 forward: register-resident update stages where they apply
 };
 constexpr int kFusedSpinLimit = 1 << 21;   // ~0.5 s of s_sleep 4 polls
 
 // Optional per-kernel timing (nrx_profile_enable): events recorded around each launch on
 // the launch stream.  Kernel ids:
-enum KernelId { K_NORM = 0, K_INIT = 1, K_UPDATE = 2, K_FUSED = 3, K_COUNT = 4 };
+enum KernelId { K_NORM = 0, K_INIT = 1, K_UPDATE = 2, K_FUSED = 3, K_UPDATE_RR = 4, K_COUNT = 5 };
 
 struct Prof {
   virtual void begin(int kid, void* stream) = 0;

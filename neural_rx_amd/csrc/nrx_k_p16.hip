@@ -6,8 +6,8 @@
 namespace nrx {
 
 hipError_t run_tier_p16(const FwdArgs<_Float16, float, _Float16>& a, const ModelW<_Float16, float>& W, int num_it,
-                       hipStream_t st, Prof* prof) {
-  return Launch<P16>::run(a, W, num_it, st, prof);
+                       hipStream_t st, Prof* prof, int update_rr) {
+  return Launch<P16>::run(a, W, num_it, st, prof, update_rr);
 }
 
 hipError_t setup_tier_p16() { return Launch<P16>::setup(); }

@@ -32,10 +32,12 @@ def launch_flops_per_re_user(spec: ModelSpec, num_it: int) -> dict:
     over its num_it launches) = state update + the next aggregation MLP, or the readouts
     after the last iteration."""
     k = kernel_flops_per_re_user(spec)
-    return {"norm": 0,
-            "state_init": k["state_init"] + k["aggregate"],
-            "state_update": k["state_update"] + ((num_it - 1) * k["aggregate"] + k["readout"]) / num_it,
-            "forward": forward_flops_per_re_user(spec, num_it)}
+    out = {"norm": 0,
+           "state_init": k["state_init"] + k["aggregate"],
+           "state_update": k["state_update"] + ((num_it - 1) * k["aggregate"] + k["readout"]) / num_it,
+           "forward": forward_flops_per_re_user(spec, num_it)}
+    out["state_update_rr"] = out["state_update"]   # the register-resident update launch: same work
+    return out
 
 
 def update_launch_bytes_per_re_user(spec: ModelSpec, num_it: int, elem: int = 2) -> float:

@@ -128,6 +128,12 @@ class CGNNEngine:
         ie = -1 if inject_err is None else int(inject_err)
         _lib.check(self._lib.nrx_fused_config(self._h, en, sl, ie))
 
+    def update_schedule(self, rr=None):
+        """Update stages of the three-launch f16 forward (include/nrx.h nrx_update_schedule): True
+        = register-resident update launch where it applies (default), False = strip kernels,
+        None = unchanged."""
+        _lib.check(self._lib.nrx_update_schedule(self._h, -1 if rr is None else int(bool(rr))))
+
     def profile_read(self):
         """{kernel: (launches, total_ms)} since the last profile(True)."""
         out = {}

@@ -1,0 +1,34 @@
+"""Slot chunks (nrx_api.cpp chunk_slots): an f16 forward whose workspace would reach the GZ
+loader's 32-bit range (1 GB) runs as consecutive sub-forwards in one chunk-sized workspace.
+Slots are independent (neural_rx.py:544-595 has no cross-slot term), so the chunked forward of
+26 slots at 273 PRB (41 MB of workspace per slot: 1.07 GB unchunked) must equal, bit for bit,
+two forwards of 13 slots each (535 MB, no chunking)."""
+import numpy as np
+import pytest
+
+from tests.helpers import make_case, run_engine
+
+pytestmark = pytest.mark.gpu
+
+
+def _sub(case, lo, hi):
+    import dataclasses
+    c = dataclasses.replace(case, y=case.y[lo:hi], h_hat=case.h_hat[lo:hi], active=case.active[lo:hi],
+                            mcs_mask=None if case.mcs_mask is None else case.mcs_mask[lo:hi])
+    return c
+
+
+def test_chunked_forward_equals_split_batches():
+    from neural_rx_amd.receiver import CGNNEngine
+    case = make_case("nrx_rt", batch=26, users=2, prbs=273, random_inputs=True, seed=61)
+    eng = CGNNEngine(case.spec, case.weights)
+    try:
+        ws = eng.workspace_bytes(26, 2, 3276)
+        assert ws < (1 << 30) and ws < 26 * 4 * 2 * 3276 * 14 * 56 * 2   # a chunk's workspace, not 26 slots'
+        full = run_engine(case, "f16", eng)
+        lo = run_engine(_sub(case, 0, 13), "f16", eng)
+        hi = run_engine(_sub(case, 13, 26), "f16", eng)
+    finally:
+        eng.close()
+    assert np.array_equal(full["llr_raw"], np.concatenate([lo["llr_raw"], hi["llr_raw"]], axis=1))
+    assert np.array_equal(full["h_hat"], np.concatenate([lo["h_hat"], hi["h_hat"]], axis=0))

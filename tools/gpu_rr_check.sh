@@ -1,0 +1,19 @@
+# RR update launch on the GPU: its tests (bit-identity vs the strip kernels, oracle), the GZ
+# boundary tests, then interleaved short bench rounds RR vs strip (NRX_UPDATE_RR=0) and a
+# kernel trace of the default bench.
+# usage (GPU box): bash tools/gpu_rr_check.sh <tag> [rounds]
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/$1; R=${2:-2}; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_update_rr.py tests/test_gpu_gz_boundary.py tests/test_gpu_chunks.py -x -v --timeout 150 --timeout-method thread > $O/pytest_rr.log 2>&1
+rc=$?; tail -4 $O/pytest_rr.log; [ $rc -eq 0 ] || exit $rc
+for r in $(seq 1 $R); do
+  for v in rr strip; do
+    if [ $v = strip ]; then E="NRX_UPDATE_RR=0"; else E="NRX_UPDATE_RR=1"; fi
+    env $E timeout -k 10 200 python bench.py --steps 400 --warmup 30 --no-cpu-baseline --no-latency --no-e2e > $O/bench_${v}_$r.json 2> $O/bench_${v}_$r.err || exit 1
+    python -c "import json; d=json.load(open('$O/bench_${v}_$r.json')); r=d['roofline']; print('$v', round(d['value']), r['avg_launch_us'], r['frac'], r['kernel'][:12])"
+  done
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python bench.py --steps 200 --warmup 20 --profile-only > $O/kt.log 2>&1 || exit 1
+find $O/kt -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-200 | head -12

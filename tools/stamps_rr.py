@@ -1,0 +1,57 @@
+"""Diagnostic: per-phase cycles of the register-resident update launch (k_update_rr), from the
+NRX_STAMPS variant library (python tools/build_variants.py stamps=-DNRX_STAMPS).
+
+usage (GPU box): NRX_STAMP_RR=<launch> python tools/stamps_rr.py [lib]
+Runs 200 bench forwards (nrx_rt, B = 128, U = 2, 4 PRB); launch 2 i is forward i's aggregation
+update, 2 i + 1 its readout update.  Prints, per item k of a workgroup (k < 4) and for waves 0
+(R = 3) and 4 (R = 2), the mean over workgroups of each phase's cycles (rr_ts in nrx_rr.inc).
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from neural_rx_amd import _lib  # noqa: E402
+
+path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(_lib.LIB_PATH), "var", "stamps", "libnrx.so")
+lib = _lib.load(path)
+lib.nrx_debug_rr_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+from neural_rx_amd import synth, weights as W  # noqa: E402
+from neural_rx_amd.config import get_config, spec_from_config  # noqa: E402
+from neural_rx_amd.receiver import CGNNEngine, compute_pe  # noqa: E402
+
+cfg = get_config("nrx_rt")
+spec = spec_from_config(cfg)
+B, U, prbs = 128, 2, 4
+sl = synth.generate(B, U, prbs, 4, [4, 4], (0, 1), snr_db=10, seed=3)
+eng = CGNNEngine(spec, W.load("nrx_rt"))
+t = lambda a: torch.from_numpy(a).cuda()
+pe = t(compute_pe(U, 48, (2, 11), (0, 1)))
+dy, dh, da = t(sl.y), t(sl.h_hat), t(sl.active)
+for _ in range(200):
+    eng.forward(dy, pe, dh, da, None, 2, "f16")
+torch.cuda.synchronize()
+n = 256
+buf = np.zeros((n, 64), np.uint64)
+lib.nrx_debug_rr_stamps(buf.ctypes.data, n)
+st = buf.astype(np.int64).reshape(n, 4, 8, 2)   # [wg][item k][m][wave 0 / 4]
+names = ["conv1", "exch1", "conv2", "exch2", "conv3", "epilogue"]
+print("launch", os.environ.get("NRX_STAMP_RR"), "(2 i: aggregation update, 2 i + 1: readout)")
+for k in range(4):
+    s0 = st[:, k, 0, 0]
+    if (s0 == 0).all():
+        continue
+    ok = s0 != 0
+    tot = st[ok, k, 6, 0] - st[ok, k, 0, 0]
+    print(f"item {k}: {ok.sum()} workgroups, item {tot.mean():.0f} cycles (wave 0)")
+    for w in (0, 1):
+        d = np.diff(st[ok, k, :7, w], axis=1)
+        print("   wave", 4 * w, "  ".join(f"{nm} {d[:, i].mean():6.0f}" for i, nm in enumerate(names)))
+if n:
+    starts = st[:, :, 0, 0]
+    ends = st[:, :, 6, 0]
+    print("kernel span (first item start -> last item end):", ends.max() - starts[starts > 0].min())
