@@ -25,7 +25,11 @@ constexpr int kAGG = 64;      // aggregation hidden width
 constexpr int kUPD_CINP = 128;  // [a, s, pe] = 114 -> 128
 constexpr int kMaxInit = 8;
 constexpr int kMaxIt = 8;
-constexpr int kInlineUsers = 4;  // users whose leave-one-out combine the update z-load forms
+// users whose leave-one-out combine the update z-load forms itself (the other user's act*sp plane
+// IS a_u for U = 2); U >= 3 runs the f32 combine pass (k_combine / combine stages) and every
+// update reads its a_u plane -- one rounding for every U > 2 and every schedule, and conv1 can
+// read a_u from memory (GZ) for any U
+constexpr int kInlineUsers = 2;
 constexpr int kMaxHeads = 8;
 constexpr int kMaxUsers = 16;
 constexpr int kHalo = 3;      // 3 stacked 3x3 convs per block

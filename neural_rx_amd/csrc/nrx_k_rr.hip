@@ -9,8 +9,11 @@ namespace nrx {
 #include "nrx_rr.inc"
 
 bool update_rr_applicable(const FwdArgs<_Float16, float, _Float16>& a, bool gz, bool inline_combine, bool last) {
+  // conv1 reads [a | s | pe] from memory: a = the other user's act*sp plane (U = 2, inline
+  // combine), none (U = 1) or the a_u plane the combine pass wrote (U > 2); see gz_make
+  (void)inline_combine;
   const int chp = 2 * a.A <= 16 ? 16 : 32;
-  if (!gz || !inline_combine || a.U > 2 || 2 * a.A > 32) return false;
+  if (!gz || 2 * a.A > 32) return false;
   return !last || (a.H == 1 && rr_heads_fit(a.bits_max, chp, 2 * a.A));
 }
 

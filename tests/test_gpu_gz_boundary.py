@@ -24,7 +24,7 @@ def test_buffer_range_check_covers_voffset_and_soffset():
     lib = _lib.load()
     lib.nrx_probe_buffer_oob.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                          ctypes.c_void_p, ctypes.c_void_p]
-    buf = torch.full((8 << 20) // 4, 0x11223344, dtype=torch.int32, device="cuda:0")   # 8 MB, marker words
+    buf = torch.full(((8 << 20) // 4,), 0x11223344, dtype=torch.int32, device="cuda:0")   # 8 MB, marker words
     out = torch.zeros(64, dtype=torch.int32, device="cuda:0")
     stream = torch.cuda.current_stream().cuda_stream
     marker = 0x11223344

@@ -90,23 +90,32 @@ def main():
         # both schedules, interleaved A B A B (the later run of a pair profits from the clock
         # state, so each keeps its better run): the one-launch forward forced on every shape it
         # applies to, and the three launches; "default" names the one nrx_forward takes
+        def took_of(prof):
+            if prof.get("forward", (0, 0))[0]:
+                return "k_forward"
+            return "three-launch rr" if prof.get("state_update_rr", (0, 0))[0] else "three-launch"
+
         eng.profile(True)
         step()
-        default_fused = eng.profile_read().get("forward", (0, 0))[0] > 0
+        default_took = took_of(eng.profile_read())
         eng.profile(False)
         res = {}
+        # three schedules: the one-launch forward (forced), three launches with the register-
+        # resident update stages (where they apply), three launches with the strip update kernels
         for _ in range(2):
-            for mode in ("force", False):
+            for mode, rr in (("force", True), (False, True), (False, False)):
                 eng.fused_config(enable=mode)
+                eng.update_schedule(rr)
                 el, prof = measure()
-                took = "k_forward" if prof.get("forward", (0, 0))[0] else "three-launch"
+                took = took_of(prof)
                 if took not in res or el < res[took][0]:
                     res[took] = (el, prof)
+        eng.update_schedule(True)
         for took, (el, prof) in res.items():
             kern = {k: {"launches": n, "avg_us": round(ms / n * 1e3, 2),
                         "tflops": round(kfl[k] * re_users / (ms / n * 1e-3) / 1e12, 1) if kfl[k] else None}
                     for k, (n, ms) in prof.items() if n}
-            row = {"config": tag, "path": took, "default": (took == "k_forward") == default_fused,
+            row = {"config": tag, "path": took, "default": took == default_took,
                    "slots_per_gpu": B, "num_it": num_it,
                    "ms_per_batch": round(el * 1e3, 4), "slots_per_s_per_gpu": round(B / el, 1),
                    "gflop_per_batch": round(fl / 1e9, 2), "whole_forward_tflops": round(fl / el / 1e12, 1),

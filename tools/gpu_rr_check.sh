@@ -1,13 +1,17 @@
 # RR update launch on the GPU: its tests (bit-identity vs the strip kernels, oracle), the GZ
-# boundary tests, then interleaved short bench rounds RR vs strip (NRX_UPDATE_RR=0) and a
-# kernel trace of the default bench.
-# usage (GPU box): bash tools/gpu_rr_check.sh <tag> [rounds]
+# boundary and slot-chunk tests, optionally the whole GPU suite, then interleaved short bench
+# rounds RR vs strip (NRX_UPDATE_RR=0) and a kernel trace of the default bench.
+# usage (GPU box): bash tools/gpu_rr_check.sh <tag> [rounds] [full]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/$1; R=${2:-2}; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu_update_rr.py tests/test_gpu_gz_boundary.py tests/test_gpu_chunks.py -x -v --timeout 150 --timeout-method thread > $O/pytest_rr.log 2>&1
 rc=$?; tail -4 $O/pytest_rr.log; [ $rc -eq 0 ] || exit $rc
+if [ "$3" = "full" ]; then
+  timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 150 --timeout-method thread > $O/pytest_gpu.log 2>&1
+  rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+fi
 for r in $(seq 1 $R); do
   for v in rr strip; do
     if [ $v = strip ]; then E="NRX_UPDATE_RR=0"; else E="NRX_UPDATE_RR=1"; fi

@@ -1,8 +1,9 @@
 """Scan gfx950 assembly for the two inline-asm hazards the compiler does not pad (DESIGN.md
 section 10, "Hazards found"): (1) a VALU write of a VGPR followed within 2 instructions by a DPP
 instruction reading it as src0 (needs 2 wait states); (2) the DPP FMAC (inline asm, the
-depthwise) writing a VGPR followed within 2 instructions by an MFMA reading it.  s_nop N counts
-as N + 1 wait states.  Linear scan per function (labels do not reset the window).
+depthwise) writing a VGPR followed by an MFMA reading it with no wait state in between.  s_nop N
+counts as N + 1 wait states, s_waitcnt as none (measured: an s_waitcnt as the only instruction
+between the two gave wrong MFMA results).  Linear scan per function (labels do not reset the window).
 
 usage: python tools/hazard_scan.py kernel.s [function-name-substring]
 """
@@ -41,6 +42,8 @@ def scan(lines, want=None):
         if op.startswith("s_nop"):
             pos += int(parts[1], 0) + 1
             continue
+        if op.startswith("s_waitcnt"):
+            continue   # no wait state: an s_waitcnt alone between the depthwise and its MFMA broke k_update_rr
         if op.startswith("s_"):
             pos += 1
             continue
