@@ -325,12 +325,14 @@ int nrx_fused_status(nrx_handle* h, int32_t* status, int32_t reset);
  * surface them; 0: none).  Any argument < 0 leaves that setting unchanged. */
 int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t inject_err);
 
-/* Update-stage schedule of the three-launch f16 forward: update_rr = 1 (default) runs the
- * register-resident update launch (layer outputs kept in registers, weights staged once per
+/* Update-stage schedule of the three-launch f16 forward, a mask: bit 0 runs the aggregation
+ * update stages (every iteration but the last), bit 1 the readout update stage (the last) as
+ * the register-resident update launch (layer outputs kept in registers, weights staged once per
  * workgroup, 16-subcarrier strips) wherever it applies -- U <= 2 with conv1 reading its rows
  * from memory, 2A <= 32, one LLR head whose readout fits -- and the strip update kernels
- * elsewhere; 0 the strip kernels everywhere; < 0 unchanged.  Outputs are bit-identical either
- * way.  The initial value comes from NRX_UPDATE_RR (0 / 1) at nrx_create. */
+ * elsewhere.  0: the strip kernels everywhere; 3: both stages; < 0 unchanged; > 3 invalid.
+ * Outputs are bit-identical either way.  The initial value comes from NRX_UPDATE_RR (0..3) at
+ * nrx_create; the default is the mask measured fastest. */
 int nrx_update_schedule(nrx_handle* h, int32_t update_rr);
 
 const char* nrx_last_error(void);

@@ -353,7 +353,7 @@ struct nrx_handle {
   int fused_enabled = 1;    // NRX_FUSED (environment, read once at nrx_create)
   int spin_limit = kFusedSpinLimit;
   int dbg_err = 0;
-  int update_rr = 1;        // nrx_update_schedule (NRX_UPDATE_RR at nrx_create)
+  int update_rr = 3;        // nrx_update_schedule (NRX_UPDATE_RR at nrx_create)
   // one-stream rule of the one-launch forward: an event the handle owns, recorded
   // behind every eager one-launch forward, stands for "that forward is done" -- the caller's
   // stream itself is never kept (it may be destroyed between calls).  last_stream is compared,
@@ -497,11 +497,10 @@ int nrx_create(const nrx_desc* desc, const float* const* weights, const int64_t*
   {
     const char* ev = getenv("NRX_UPDATE_RR");   // A/B: 0 = strip update kernels
     if (ev && *ev) {
-      if (!strcmp(ev, "0")) h->update_rr = 0;
-      else if (!strcmp(ev, "1")) h->update_rr = 1;
+      if (ev[0] >= '0' && ev[0] <= '3' && !ev[1]) h->update_rr = ev[0] - '0';
       else {
         delete h;
-        return fail(NRX_ERR_INVALID_ARG, std::string("NRX_UPDATE_RR must be 0 or 1, got '") + ev + "'");
+        return fail(NRX_ERR_INVALID_ARG, std::string("NRX_UPDATE_RR must be a stage mask 0..3, got '") + ev + "'");
       }
     }
   }
@@ -906,7 +905,8 @@ int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t 
 
 int nrx_update_schedule(nrx_handle* h, int32_t update_rr) {
   if (!h) return fail(NRX_ERR_INVALID_ARG, "null argument");
-  if (update_rr >= 0) h->update_rr = update_rr ? 1 : 0;
+  if (update_rr > 3) return fail(NRX_ERR_INVALID_ARG, "update_rr is a stage mask 0..3");
+  if (update_rr >= 0) h->update_rr = update_rr;
   return NRX_OK;
 }
 

@@ -124,7 +124,7 @@ struct FusedCtl {
   int enabled;   // 0 off, 1 where measured faster (the bench-type schedule), 2 every applicable shape
   int spin_limit;
   int dbg_err;
-  int update_rr;   // three-launch f16 forward: register-resident update stages where they apply
+  int update_rr;   // three-launch f16 forward: stage mask (1 aggregation, 2 readout) run register-resident
 };
 constexpr int kFusedSpinLimit = 1 << 21;   // ~0.5 s of s_sleep 4 polls
 

@@ -129,10 +129,12 @@ class CGNNEngine:
         _lib.check(self._lib.nrx_fused_config(self._h, en, sl, ie))
 
     def update_schedule(self, rr=None):
-        """Update stages of the three-launch f16 forward (include/nrx.h nrx_update_schedule): True
-        = register-resident update launch where it applies (default), False = strip kernels,
-        None = unchanged."""
-        _lib.check(self._lib.nrx_update_schedule(self._h, -1 if rr is None else int(bool(rr))))
+        """Update stages of the three-launch f16 forward (include/nrx.h nrx_update_schedule): a
+        stage mask (bit 0 the aggregation updates, bit 1 the readout update) run as the
+        register-resident update launch where it applies; True = 3, False = 0 (strip kernels
+        everywhere), None = unchanged."""
+        m = -1 if rr is None else 3 if rr is True else 0 if rr is False else int(rr)
+        _lib.check(self._lib.nrx_update_schedule(self._h, m))
 
     def profile_read(self):
         """{kernel: (launches, total_ms)} since the last profile(True)."""

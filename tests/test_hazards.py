@@ -1,27 +1,35 @@
-"""The register-resident update kernel's depthwise (inline-asm DPP FMACs) must never feed an MFMA
-without a wait state in between (tools/hazard_scan.py; DESIGN.md section 14: an s_waitcnt alone
-between the two gave wrong B operands).  Compiles nrx_k_rr.hip to gfx950 assembly (~20 s) and
-scans it; skipped where hipcc is absent."""
+"""No inline-asm depthwise result (DPP FMAC) may feed an MFMA without a wait state in between
+(tools/hazard_scan.py; DESIGN.md section 14: an s_waitcnt alone between the two gave the RR kernel
+wrong B operands).  Compiles every kernel translation unit to gfx950 assembly in parallel (~2 min
+on 8 cores) and scans it; skipped where hipcc is absent."""
 import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TUS = ["nrx_k_rr.hip", "nrx_k_p16.hip", "nrx_k_p16m.hip", "nrx_k_p16s.hip", "nrx_k_fwd0.hip", "nrx_k_fwd1.hip",
+       "nrx_k_fwd2.hip"]
 
 
-def test_rr_kernel_has_no_dpp_mfma_hazard(tmp_path):
+def test_no_dpp_mfma_hazard(tmp_path):
     hipcc = "/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else shutil.which("hipcc")
     if not hipcc:
         pytest.skip("hipcc not available")
-    out = tmp_path / "rr.s"
-    src = os.path.join(ROOT, "neural_rx_amd", "csrc", "nrx_k_rr.hip")
-    subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "--offload-device-only", "-S",
-                    "-o", str(out), src], check=True, capture_output=True)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import hazard_scan
-    hits = hazard_scan.scan(out.read_text().splitlines(), "k_update_rr")
-    adjacent = [h for h in hits if h[1].endswith("d=1")]
-    assert not adjacent, adjacent[:5]
+
+    def one(tu):
+        out = tmp_path / (tu + ".s")
+        src = os.path.join(ROOT, "neural_rx_amd", "csrc", tu)
+        subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "--offload-device-only", "-S",
+                        "-o", str(out), src], check=True, capture_output=True)
+        hits = hazard_scan.scan(out.read_text().splitlines())
+        return tu, [h for h in hits if h[1].endswith("d=1")]
+
+    with ThreadPoolExecutor(min(len(TUS), os.cpu_count() or 4)) as ex:
+        for tu, adjacent in ex.map(one, TUS):
+            assert not adjacent, (tu, adjacent[:5])

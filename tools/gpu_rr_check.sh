@@ -1,6 +1,6 @@
 # RR update launch on the GPU: its tests (bit-identity vs the strip kernels, oracle), the GZ
 # boundary and slot-chunk tests, optionally the whole GPU suite, then interleaved short bench
-# rounds RR vs strip (NRX_UPDATE_RR=0) and a kernel trace of the default bench.
+# rounds over the stage masks NRX_UPDATE_RR=0..3 and kernel traces of masks 0 (strip) and 3 (RR).
 # usage (GPU box): bash tools/gpu_rr_check.sh <tag> [rounds] [full]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -13,11 +13,13 @@ if [ "$3" = "full" ]; then
   rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 fi
 for r in $(seq 1 $R); do
-  for v in rr strip; do
-    if [ $v = strip ]; then E="NRX_UPDATE_RR=0"; else E="NRX_UPDATE_RR=1"; fi
-    env $E timeout -k 10 200 python bench.py --steps 400 --warmup 30 --no-cpu-baseline --no-latency --no-e2e > $O/bench_${v}_$r.json 2> $O/bench_${v}_$r.err || exit 1
-    python -c "import json; d=json.load(open('$O/bench_${v}_$r.json')); r=d['roofline']; print('$v', round(d['value']), r['avg_launch_us'], r['frac'], r['kernel'][:12])"
+  for m in 0 1 2 3; do
+    NRX_UPDATE_RR=$m timeout -k 10 200 python bench.py --steps 400 --warmup 30 --no-cpu-baseline --no-latency --no-e2e > $O/bench_m${m}_$r.json 2> $O/bench_m${m}_$r.err || exit 1
+    python -c "import json; d=json.load(open('$O/bench_m${m}_$r.json')); r=d['roofline']; print('mask $m', round(d['value']), r['avg_launch_us'], r['frac'], r['kernel'][:12])"
   done
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python bench.py --steps 200 --warmup 20 --profile-only > $O/kt.log 2>&1 || exit 1
-find $O/kt -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-200 | head -12
+# per-kernel durations of the strip (mask 0) and RR (mask 3) schedules
+for m in 0 3; do
+  NRX_UPDATE_RR=$m timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt$m -o run --output-format csv -- python bench.py --steps 200 --warmup 20 --profile-only > $O/kt$m.log 2>&1 || exit 1
+  echo "mask $m"; find $O/kt$m -name "*kernel_stats.csv" -exec cat {} \; | cut -d, -f1-4 | cut -c1-150 | head -8
+done

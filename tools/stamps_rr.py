@@ -51,7 +51,19 @@ for k in range(4):
     for w in (0, 1):
         d = np.diff(st[ok, k, :7, w], axis=1)
         print("   wave", 4 * w, "  ".join(f"{nm} {d[:, i].mean():6.0f}" for i, nm in enumerate(names)))
-if n:
-    starts = st[:, :, 0, 0]
-    ends = st[:, :, 6, 0]
-    print("kernel span (first item start -> last item end):", ends.max() - starts[starts > 0].min())
+stage = st[:, 0, 0, 0] - st[:, 0, 7, 0]
+ok = (st[:, 0, 7, 0] != 0) & (st[:, 0, 0, 0] != 0)
+if ok.any():
+    print(f"weight staging (kernel start -> item 0 start, wave 0): mean {stage[ok].mean():.0f} max {stage[ok].max()} cycles")
+rt0, rt1, mt1, mt0 = buf[:, 16 + 14].astype(np.int64), buf[:, 32 + 14].astype(np.int64), \
+    buf[:, 48 + 14].astype(np.int64), buf[:, 14].astype(np.int64)
+ok = (rt0 > 0) & (rt1 > 0)
+if ok.any():
+    # s_memrealtime runs at 100 MHz on every XCD; s_memtime is the XCD's own shader clock
+    span = (rt1[ok].max() - rt0[ok].min()) / 100.0
+    per = (rt1[ok] - rt0[ok]) / 100.0
+    mhz = (mt1[ok] - mt0[ok]) / np.maximum(per, 1e-3)
+    print(f"kernel wall span {span:.2f} us (first workgroup start -> last end); per workgroup "
+          f"{per.mean():.2f} us mean, {per.min():.2f} min, {per.max():.2f} max; start skew "
+          f"{(rt0[ok].max() - rt0[ok].min()) / 100.0:.2f} us; shader clock {mhz.mean():.0f} MHz "
+          f"(min {mhz.min():.0f}, max {mhz.max():.0f})")
