@@ -250,9 +250,18 @@ def main():
                           "tflops": round(fl / avg_s / 1e12, 2) if fl else None}
     fused = prof.get("forward", (0, 0.0))[0] > 0
     # the dominant kernel: the one-launch forward when the engine took it (throughput tier),
-    # else the state-update launch of the three-launch forward
-    dom = "forward" if fused else ("state_update_rr" if prof.get("state_update_rr", (0, 0.0))[0] else "state_update")
-    dom_avg_s = prof[dom][1] / prof[dom][0] * 1e-3 * scale
+    # else the state-update launches of the three-launch forward, whichever kernel ran each
+    # stage (nrx_update_schedule: the RR launch for the aggregation updates and the strip
+    # k_update for the readout update by default) -- averaged over all update launches, as
+    # kflops["state_update"] is the average work of one update launch
+    if fused:
+        dom, upd = "forward", ["forward"]
+    else:
+        upd = [k for k in ("state_update_rr", "state_update") if prof.get(k, (0, 0.0))[0]]
+        dom = "state_update"
+    dom_n = sum(prof[k][0] for k in upd)
+    dom_ms = sum(prof[k][1] for k in upd)
+    dom_avg_s = dom_ms / dom_n * 1e-3 * scale
     dom_flops = kflops[dom] * re_users
     peak = metrics.PEAK_TFLOPS[args.precision]
     achieved = dom_flops / dom_avg_s / 1e12
@@ -270,9 +279,10 @@ def main():
                       "f16 MFMA peak, pipes overlapped (metrics.forward_mixed_bound_tflops)")
     else:
         alg_bytes = metrics.update_launch_bytes_per_re_user(spec, num_it, elem) * re_users
+        names = {"state_update_rr": "k_update_rr (register-resident)", "state_update": "k_update (strip)"}
+        split = ", ".join(f"{names[k]} x {prof[k][0] // args.steps}" for k in upd)
         pmc_field, kname = "k_update_bytes_per_launch", (
-            "k_update_rr (register-resident update launch: 3 sep-convs + fused aggregation/readout tail)"
-            if dom == "state_update_rr" else "k_update (3 sep-convs + fused aggregation/readout tail)")
+            f"update stage (3 sep-convs + fused aggregation/readout tail; per forward: {split})")
         mixed = metrics.mixed_bound_tflops(spec, num_it, peak) if args.precision == "f16" else None
         mixed_note = ("k_update's depthwise FLOPs at the VALU peak (157 TF) + its dense FLOPs at the f16 "
                       "MFMA peak, pipes overlapped (metrics.mixed_bound_tflops)")
@@ -328,7 +338,7 @@ def main():
                 "wait_frac": sq.get("wait_frac"),
                 "sq_source": sq.get("source"),
                 "avg_launch_us": round(dom_avg_s * 1e6, 3),
-                "avg_launch_us_event_pairs": kern[dom]["avg_us_event_pairs"],
+                "avg_launch_us_event_pairs": round(dom_ms / dom_n * 1e3, 3),
                 "avg_launch_us_kind": "derived: event-pair share of a step x uninstrumented step time",
                 "event_pair_scale": round(scale, 5),
                 "uninstrumented_step_ms": round(stream_step_ms, 5),

@@ -284,7 +284,8 @@ double nrx_flops_per_re_user(const nrx_desc* desc, int32_t num_it);
  * 0 norm, 1 state-init (+ fused aggregation tail), 2 state-update (+ fused aggregation
  * or readout tail), 3 the one-launch forward (StateInit + updates + readouts; see
  * nrx_fused_status for when it is taken), 4 the register-resident state-update launch
- * (nrx_update_schedule).
+ * (nrx_update_schedule), 5 the leave-one-out combine pass of U > 2 users (k_combine: after
+ * StateInit and after every aggregation update).
  * nrx_profile_enable(h, 1) (re)starts the counters; nrx_profile_read waits for the
  * recorded events and returns the launch count and summed device time of a kernel. */
 int nrx_profile_enable(nrx_handle* h, int32_t enable);

@@ -32,7 +32,7 @@ EXPORTS = [
 ]
 # enum nrx_y_layout
 Y_LAYOUTS = {"cgnn": 0, "sionna": 1, "split": 2}
-KERNELS = ["norm", "state_init", "state_update", "forward", "state_update_rr"]
+KERNELS = ["norm", "state_init", "state_update", "forward", "state_update_rr", "combine"]
 
 
 class NRXLibraryError(RuntimeError):

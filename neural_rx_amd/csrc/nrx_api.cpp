@@ -353,7 +353,7 @@ struct nrx_handle {
   int fused_enabled = 1;    // NRX_FUSED (environment, read once at nrx_create)
   int spin_limit = kFusedSpinLimit;
   int dbg_err = 0;
-  int update_rr = 3;        // nrx_update_schedule (NRX_UPDATE_RR at nrx_create)
+  int update_rr = 1;        // nrx_update_schedule (NRX_UPDATE_RR at nrx_create)
   // one-stream rule of the one-launch forward: an event the handle owns, recorded
   // behind every eager one-launch forward, stands for "that forward is done" -- the caller's
   // stream itself is never kept (it may be destroyed between calls).  last_stream is compared,

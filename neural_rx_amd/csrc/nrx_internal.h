@@ -130,7 +130,7 @@ constexpr int kFusedSpinLimit = 1 << 21;   // ~0.5 s of s_sleep 4 polls
 
 // Optional per-kernel timing (nrx_profile_enable): events recorded around each launch on
 // the launch stream.  Kernel ids:
-enum KernelId { K_NORM = 0, K_INIT = 1, K_UPDATE = 2, K_FUSED = 3, K_UPDATE_RR = 4, K_COUNT = 5 };
+enum KernelId { K_NORM = 0, K_INIT = 1, K_UPDATE = 2, K_FUSED = 3, K_UPDATE_RR = 4, K_COMBINE = 5, K_COUNT = 6 };
 
 struct Prof {
   virtual void begin(int kid, void* stream) = 0;

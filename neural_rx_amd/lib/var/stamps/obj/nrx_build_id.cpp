@@ -1,1 +1,1 @@
-extern "C" const char* nrx_build_id(void) { return "0b900a55479a3e5a+-DNRX_STAMPS"; }
+extern "C" const char* nrx_build_id(void) { return "fb63bf08e13a69f6+-DNRX_STAMPS"; }

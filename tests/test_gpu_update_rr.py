@@ -2,8 +2,8 @@
 
 Every MFMA of k_update_rr sees the operands of the strip kernel's GZ items in the same order, so
 its outputs must equal the strip update kernels' bit for bit: each case runs the three-launch
-f16 forward twice on one engine, update_schedule(False) (strip k_update) and update_schedule(True)
-(k_update_rr), checks from the per-launch profile that the intended kernel ran, compares LLRs and
+f16 forward twice on one engine, update_schedule(0) (strip k_update) and a stage mask (default 3:
+k_update_rr for every update stage), checks from the per-launch profile that the intended kernel ran, compares LLRs and
 h_ref exactly, and the RR result against the fp64 oracle within the f16 gate of
 tests/test_gpu_parity.py."""
 import numpy as np
@@ -35,16 +35,16 @@ def _run(case, rr):
         prof = eng.profile_read()
         eng.profile(False)
     finally:
-        eng.update_schedule(True)
+        eng.update_schedule(1)          # the library default: register-resident aggregation updates
         eng.fused_config(enable=True)
     return out, prof
 
 
-def _check(case, oracle=True, rr_launches=None):
+def _check(case, oracle=True, rr_launches=None, mask=3):
     n_it = case.num_it or case.spec.num_it
     rr_launches = n_it if rr_launches is None else rr_launches
-    ref, pr = _run(case, False)
-    got, pg = _run(case, True)
+    ref, pr = _run(case, 0)
+    got, pg = _run(case, mask)
     assert pr["state_update_rr"][0] == 0 and pr["state_update"][0] == n_it
     assert pg["state_update_rr"][0] == rr_launches and pg["state_update"][0] == n_it - rr_launches, pg
     assert np.array_equal(ref["llr_raw"], got["llr_raw"]), np.abs(ref["llr_raw"] - got["llr_raw"]).max()
@@ -87,3 +87,14 @@ def test_rr_var_io_three_launch():
     case = make_case("nrx_rt_var_mcs", batch=128, users=2, prbs=4, snr_db=14, seed=55,
                      mcs_choice=rng.integers(0, 2, size=(128, 2)))
     _check(case, oracle=False, rr_launches=case.spec.num_it - 1)
+
+
+@pytest.mark.parametrize("mask", [1, 2])
+def test_rr_stage_masks(mask):
+    # nrx_update_schedule is a stage mask: 1 (the default) the aggregation updates only, 2 the
+    # readout update only; the other stages run the strip kernel, outputs unchanged
+    # (nrx_large topology: 8 iterations, so 7 aggregation updates and one readout update; B = 128
+    # so that the grid takes the 24-row strip tier, the one with the RR launch)
+    case = make_case("nrx_large", batch=128, users=2, prbs=4, seeded_weights=True, random_inputs=True, seed=56)
+    n_it = case.num_it or case.spec.num_it
+    _check(case, oracle=False, rr_launches=n_it - 1 if mask == 1 else 1, mask=mask)

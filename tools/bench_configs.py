@@ -101,16 +101,17 @@ def main():
         eng.profile(False)
         res = {}
         # three schedules: the one-launch forward (forced), three launches with the register-
-        # resident update stages (where they apply), three launches with the strip update kernels
+        # resident aggregation updates (the default mask 1, where they apply), three launches with
+        # the strip update kernels
         for _ in range(2):
-            for mode, rr in (("force", True), (False, True), (False, False)):
+            for mode, rr in (("force", 1), (False, 1), (False, 0)):   # rr: nrx_update_schedule mask
                 eng.fused_config(enable=mode)
                 eng.update_schedule(rr)
                 el, prof = measure()
                 took = took_of(prof)
                 if took not in res or el < res[took][0]:
                     res[took] = (el, prof)
-        eng.update_schedule(True)
+        eng.update_schedule(1)
         for took, (el, prof) in res.items():
             kern = {k: {"launches": n, "avg_us": round(ms / n * 1e3, 2),
                         "tflops": round(kfl[k] * re_users / (ms / n * 1e-3) / 1e12, 1) if kfl[k] else None}
