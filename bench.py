@@ -162,8 +162,11 @@ def main():
     y, h, act, pe = t(slots.y), t(slots.h_hat), t(slots.active), t(pe_np)
     out = eng.alloc_outputs(B, U, F)
 
+    fwd_count = [0]   # forwards executed (--profile-only reports it: PMC records per forward)
+
     def step_eager():
         eng.forward(y, pe, h, act, None, num_it, args.precision, out=out)
+        fwd_count[0] += 1
 
     # The timed steps are direct nrx_forward calls (async, no host sync: the host runs ahead
     # of the device); --graph replays one captured forward instead (measured slower at this
@@ -180,7 +183,11 @@ def main():
         with torch.cuda.graph(graph, stream=graph_stream):
             step_eager()
         torch.cuda.synchronize()
-        step = graph.replay
+        fwd_count[0] -= 1   # captured, not executed
+
+        def step():
+            graph.replay()
+            fwd_count[0] += 1
 
     # Steady state: the GPU takes tens of ms of back-to-back work to reach its load clock
     # (a fresh box measured 768 k slots/s with only the W = 5 warmup steps before 20 timed
@@ -216,7 +223,8 @@ def main():
         elapsed = float(e.item())
     if args.profile_only:
         if rank == 0:
-            print(json.dumps({"profile_only": True, "ms_per_step": 1e3 * elapsed / args.steps}))
+            print(json.dumps({"profile_only": True, "ms_per_step": 1e3 * elapsed / args.steps,
+                              "forwards": fwd_count[0]}))
         if world > 1:
             dist.destroy_process_group()
         return

@@ -13,12 +13,12 @@ if [ "$3" = "full" ]; then
   rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 fi
 for r in $(seq 1 $R); do
-  for m in 0 1 2 3; do
+  for m in ${MASKS:-0 1 2 3}; do
     NRX_UPDATE_RR=$m timeout -k 10 200 python bench.py --steps 400 --warmup 30 --no-cpu-baseline --no-latency --no-e2e > $O/bench_m${m}_$r.json 2> $O/bench_m${m}_$r.err || exit 1
     python -c "import json; d=json.load(open('$O/bench_m${m}_$r.json')); r=d['roofline']; print('mask $m', round(d['value']), r['avg_launch_us'], r['frac'], r['kernel'][:12])"
   done
-  for v in $VARS; do   # variant libraries (tools/build_variants.py), mask 3
-    NRX_LIB_PATH=neural_rx_amd/lib/var/$v/libnrx.so NRX_UPDATE_RR=3 timeout -k 10 200 python bench.py --steps 400 --warmup 30 --no-cpu-baseline --no-latency --no-e2e > $O/bench_${v}_$r.json 2> $O/bench_${v}_$r.err || exit 1
+  for v in $VARS; do   # variant libraries (tools/build_variants.py), mask $VMASK (default 1)
+    NRX_LIB_PATH=neural_rx_amd/lib/var/$v/libnrx.so NRX_UPDATE_RR=${VMASK:-1} timeout -k 10 200 python bench.py --steps 400 --warmup 30 --no-cpu-baseline --no-latency --no-e2e > $O/bench_${v}_$r.json 2> $O/bench_${v}_$r.err || exit 1
     python -c "import json; d=json.load(open('$O/bench_${v}_$r.json')); r=d['roofline']; print('var $v', round(d['value']), r['avg_launch_us'], r['frac'], r['kernel'][:12])"
   done
 done

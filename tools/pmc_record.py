@@ -56,6 +56,19 @@ def dispatch_counts(dirs):
     return {}
 
 
+def forwards_run(dirs):
+    """forwards the profiled bench run executed: bench.py --profile-only prints them in the
+    pass's log (<dir>.log); a forward split into slot chunks runs one k_init per chunk, so
+    counting k_init dispatches would report per-chunk bytes"""
+    for d in dirs:
+        log = d.rstrip("/") + ".log"
+        if os.path.exists(log):
+            for line in open(log):
+                if line.startswith("{") and '"forwards"' in line:
+                    return json.loads(line)["forwards"]
+    return 0
+
+
 def running_build_id():
     """nrx_build_id() of the in-tree libnrx.so -- the library the passes just profiled"""
     sys.path.insert(0, ROOT)
@@ -101,9 +114,9 @@ def main(key, source, dirs, cus=256):
     if not fwd:
         # three-launch forward (e.g. cfg5's per-GPU shard, U = 8): every kernel's bytes per
         # dispatch, and the forward's total = sum over kernels of mean x dispatches per forward
-        # (forwards = k_init dispatches: one StateInit per forward for these models)
+        # (forwards = the count bench.py --profile-only logged, else k_init dispatches)
         cnt = dispatch_counts(dirs)
-        n_fwd = max((v for k, v in cnt.items() if k.startswith("nrx::k_init")), default=0)
+        n_fwd = forwards_run(dirs) or max((v for k, v in cnt.items() if k.startswith("nrx::k_init")), default=0)
         kern, tot = {}, 0.0
         for k, cs in pk.items():
             if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs and k.startswith("nrx::"):

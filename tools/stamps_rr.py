@@ -10,6 +10,8 @@ import ctypes
 import os
 import sys
 
+os.environ.setdefault("NRX_UPDATE_RR", "3")   # both update stages register-resident: launches 2 i, 2 i + 1
+
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
