@@ -98,3 +98,17 @@ def test_rr_stage_masks(mask):
     case = make_case("nrx_large", batch=128, users=2, prbs=4, seeded_weights=True, random_inputs=True, seed=56)
     n_it = case.num_it or case.spec.num_it
     _check(case, oracle=False, rr_launches=n_it - 1 if mask == 1 else 1, mask=mask)
+
+
+def test_rr_one_prb_strip_past_the_grid():
+    # F = 12 < 16: the only strip's rows 12..18 lie past the grid (zeroed behind the uniform
+    # branch of rr_to_own); U = 1, B = 640 so that the 24-row tier (and the RR launch) is taken
+    case = make_case("nrx_rt", batch=640, users=1, prbs=1, snr_db=12, seed=57)
+    _check(case)
+
+
+def test_rr_three_users_combine_pass():
+    # U = 3: conv1 reads the a_u planes k_combine wrote (GZ), both update stages register-resident
+    case = make_case("nrx_rt", batch=128, users=3, prbs=4, snr_db=12, seed=58,
+                     active=np.random.default_rng(58).integers(0, 2, size=(128, 3)).astype(np.float32))
+    _check(case)
