@@ -112,3 +112,12 @@ def test_rr_three_users_combine_pass():
     case = make_case("nrx_rt", batch=128, users=3, prbs=4, snr_db=12, seed=58,
                      active=np.random.default_rng(58).integers(0, 2, size=(128, 3)).astype(np.float32))
     _check(case)
+
+
+@pytest.mark.parametrize("users", [4, 8])
+def test_rr_users_4_8_combine_pass(users):
+    # U = 4 / 8: conv1 of every RR item reads the a_u planes k_combine wrote (GZ); outputs must
+    # equal the strip kernels' bit for bit, with random activity (p = 1/(n-1) varies per slot)
+    case = make_case("nrx_rt", batch=64, users=users, prbs=4, snr_db=12, seed=59 + users,
+                     active=np.random.default_rng(59 + users).integers(0, 2, size=(64, users)).astype(np.float32))
+    _check(case, oracle=users == 4)

@@ -26,13 +26,15 @@ from neural_rx_amd import synth, weights as W  # noqa: E402
 from neural_rx_amd.config import get_config, spec_from_config  # noqa: E402
 from neural_rx_amd.receiver import CGNNEngine, compute_pe  # noqa: E402
 
+# NRX_STAMP_SHAPE = "B,U,PRB" (nrx_rt weights; default the bench shape 128,2,4)
+B, U, prbs = (int(x) for x in os.environ.get("NRX_STAMP_SHAPE", "128,2,4").split(","))
 cfg = get_config("nrx_rt")
 spec = spec_from_config(cfg)
-B, U, prbs = 128, 2, 4
-sl = synth.generate(B, U, prbs, 4, [4, 4], (0, 1), snr_db=10, seed=3)
+groups = tuple(i % 2 for i in range(U))
+sl = synth.generate(B, U, prbs, 4, [4] * U, groups, snr_db=10, seed=3)
 eng = CGNNEngine(spec, W.load("nrx_rt"))
 t = lambda a: torch.from_numpy(a).cuda()
-pe = t(compute_pe(U, 48, (2, 11), (0, 1)))
+pe = t(compute_pe(U, 12 * prbs, (2, 11), groups))
 dy, dh, da = t(sl.y), t(sl.h_hat), t(sl.active)
 for _ in range(200):
     eng.forward(dy, pe, dh, da, None, 2, "f16")
