@@ -32,3 +32,23 @@ def test_chunked_forward_equals_split_batches():
         eng.close()
     assert np.array_equal(full["llr_raw"], np.concatenate([lo["llr_raw"], hi["llr_raw"]], axis=1))
     assert np.array_equal(full["h_hat"], np.concatenate([lo["h_hat"], hi["h_hat"]], axis=0))
+
+
+def test_chunked_forward_eight_users_combine_pass():
+    # U = 8 (the combine pass between stages, RR aggregation updates): 8 slots at 273 PRB need
+    # 1.3 GB unchunked and run as chunks; the result must equal forwards of 4 + 4 slots (random
+    # activity, so the combine's 1/(n-1) differs per slot and chunk boundaries would show)
+    from neural_rx_amd.receiver import CGNNEngine
+    rng = np.random.default_rng(62)
+    case = make_case("nrx_rt", batch=8, users=8, prbs=273, random_inputs=True, seed=62,
+                     active=rng.integers(0, 2, size=(8, 8)).astype(np.float32))
+    eng = CGNNEngine(case.spec, case.weights)
+    try:
+        assert eng.workspace_bytes(8, 8, 3276) < (1 << 30)
+        full = run_engine(case, "f16", eng)
+        lo = run_engine(_sub(case, 0, 4), "f16", eng)
+        hi = run_engine(_sub(case, 4, 8), "f16", eng)
+    finally:
+        eng.close()
+    assert np.array_equal(full["llr_raw"], np.concatenate([lo["llr_raw"], hi["llr_raw"]], axis=1))
+    assert np.array_equal(full["h_hat"], np.concatenate([lo["h_hat"], hi["h_hat"]], axis=0))
