@@ -329,8 +329,9 @@ int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t 
 /* Update-stage schedule of the three-launch f16 forward, a mask: bit 0 runs the aggregation
  * update stages (every iteration but the last), bit 1 the readout update stage (the last) as
  * the register-resident update launch (layer outputs kept in registers, weights staged once per
- * workgroup, 16-subcarrier strips) wherever it applies -- U <= 2 with conv1 reading its rows
- * from memory, 2A <= 32, one LLR head whose readout fits -- and the strip update kernels
+ * workgroup, 16-subcarrier strips) wherever it applies -- the 24-row strip tier with conv1
+ * reading its rows from memory (any U: for U > 2 the combine pass's a_u planes), 2A <= 32, for
+ * the readout stage one LLR head whose readout fits -- and the strip update kernels
  * elsewhere.  0: the strip kernels everywhere; 3: both stages; < 0 unchanged; > 3 invalid.
  * Outputs are bit-identical either way.  The initial value comes from NRX_UPDATE_RR (0..3) at
  * nrx_create; the default is the mask measured fastest. */
