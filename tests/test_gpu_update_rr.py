@@ -121,3 +121,23 @@ def test_rr_users_4_8_combine_pass(users):
     case = make_case("nrx_rt", batch=64, users=users, prbs=4, snr_db=12, seed=59 + users,
                      active=np.random.default_rng(59 + users).integers(0, 2, size=(64, users)).astype(np.float32))
     _check(case, oracle=users == 4)
+
+
+def test_update_schedule_mask_validation(monkeypatch):
+    # nrx_update_schedule takes a stage mask 0..3 (< 0: unchanged); NRX_UPDATE_RR must be one
+    # digit 0..3 or nrx_create fails (no silent fallback to a schedule the caller did not ask for)
+    from neural_rx_amd import _lib
+    from neural_rx_amd.receiver import CGNNEngine
+    case = make_case("nrx_rt", batch=2, users=2, prbs=4, seed=63)
+    eng = CGNNEngine(case.spec, case.weights)
+    try:
+        for m in (0, 1, 2, 3, -1, True, False, None):
+            eng.update_schedule(m)
+        with pytest.raises(_lib.NRXError):
+            eng.update_schedule(4)
+    finally:
+        eng.close()
+    for bad in ("4", "on", "13"):
+        monkeypatch.setenv("NRX_UPDATE_RR", bad)
+        with pytest.raises(_lib.NRXError):
+            CGNNEngine(case.spec, case.weights)
