@@ -265,7 +265,7 @@ def main():
     if fused:
         dom, upd = "forward", ["forward"]
     else:
-        upd = [k for k in ("state_update_rr", "state_update") if prof.get(k, (0, 0.0))[0]]
+        upd = [k for k in ("state_update_col", "state_update_rr", "state_update") if prof.get(k, (0, 0.0))[0]]
         dom = "state_update"
     dom_n = sum(prof[k][0] for k in upd)
     dom_ms = sum(prof[k][1] for k in upd)
@@ -287,7 +287,8 @@ def main():
                       "f16 MFMA peak, pipes overlapped (metrics.forward_mixed_bound_tflops)")
     else:
         alg_bytes = metrics.update_launch_bytes_per_re_user(spec, num_it, elem) * re_users
-        names = {"state_update_rr": "k_update_rr (register-resident)", "state_update": "k_update (strip)"}
+        names = {"state_update_col": "k_update_col (whole-column)", "state_update_rr": "k_update_rr (register-resident)",
+                 "state_update": "k_update (strip)"}
         split = ", ".join(f"{names[k]} x {prof[k][0] // args.steps}" for k in upd)
         pmc_field, kname = "k_update_bytes_per_launch", (
             f"update stage (3 sep-convs + fused aggregation/readout tail; per forward: {split})")

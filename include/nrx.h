@@ -285,7 +285,8 @@ double nrx_flops_per_re_user(const nrx_desc* desc, int32_t num_it);
  * or readout tail), 3 the one-launch forward (StateInit + updates + readouts; see
  * nrx_fused_status for when it is taken), 4 the register-resident state-update launch
  * (nrx_update_schedule), 5 the leave-one-out combine pass of U > 2 users (k_combine: after
- * StateInit and after every aggregation update).
+ * StateInit and after every aggregation update), 6 the whole-column state-update launch, 7 the
+ * whole-column StateInit launch (nrx_update_schedule).
  * nrx_profile_enable(h, 1) (re)starts the counters; nrx_profile_read waits for the
  * recorded events and returns the launch count and summed device time of a kernel. */
 int nrx_profile_enable(nrx_handle* h, int32_t enable);
@@ -326,15 +327,22 @@ int nrx_fused_status(nrx_handle* h, int32_t* status, int32_t reset);
  * surface them; 0: none).  Any argument < 0 leaves that setting unchanged. */
 int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t inject_err);
 
-/* Update-stage schedule of the three-launch f16 forward, a mask: bit 0 runs the aggregation
- * update stages (every iteration but the last), bit 1 the readout update stage (the last) as
- * the register-resident update launch (layer outputs kept in registers, weights staged once per
- * workgroup, 16-subcarrier strips) wherever it applies -- the 24-row strip tier with conv1
- * reading its rows from memory (any U: for U > 2 the combine pass's a_u planes), 2A <= 32, for
- * the readout stage one LLR head whose readout fits -- and the strip update kernels
- * elsewhere.  0: the strip kernels everywhere; 3: both stages; < 0 unchanged; > 3 invalid.
- * Outputs are bit-identical either way.  The initial value comes from NRX_UPDATE_RR (0..3) at
- * nrx_create; the default is the mask measured fastest. */
+/* Stage schedule of the three-launch f16 forward, a mask (24-row strip tier):
+ *   bit 0 (1)  the aggregation update stages (every iteration but the last) and
+ *   bit 1 (2)  the readout update stage (the last) as the register-resident 16-row launch
+ *              (k_update_rr: layer outputs kept in registers, weights staged once per workgroup);
+ *   bit 2 (4)  the aggregation update stages and
+ *   bit 3 (8)  the readout update stage as the whole-column launch (k_update_col: 48-position
+ *              items, 6 register-resident rows per wave, no halo on grids of <= 48 subcarriers;
+ *              taken over bits 0 / 1);
+ *   bit 4 (16) StateInit as the whole-column launch (k_init_col: one StateInit, 2A = 8).
+ * Each applies where it can -- the update launches with conv1 reading its rows from memory (any
+ * U: for U > 2 the combine pass's a_u planes), 2A <= 32, for the readout stage one LLR head
+ * whose readout fits -- the strip kernels elsewhere.  0: the strip kernels everywhere; < 0
+ * unchanged; > 31 invalid.  Outputs are bit-identical either way.  The initial value comes from
+ * NRX_UPDATE_RR (0..31) at nrx_create; the default (29: every column stage, the RR aggregation
+ * update where the column one does not apply) is the mask measured fastest.
+ * Kernel ids 6 / 7 of nrx_profile_read time the column update / StateInit launches. */
 int nrx_update_schedule(nrx_handle* h, int32_t update_rr);
 
 const char* nrx_last_error(void);

@@ -14,6 +14,7 @@ LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("NRX_LIB_PATH") or os.path.join(LIB_DIR, "libnrx.so")
 
 NRX_OK = 0
+NRX_ERR_INVALID_ARG = -1
 NRX_ERR_BUSY = -7
 NRX_ERR_FUSED = -8
 NRX_PREC_F16 = 0
@@ -32,7 +33,8 @@ EXPORTS = [
 ]
 # enum nrx_y_layout
 Y_LAYOUTS = {"cgnn": 0, "sionna": 1, "split": 2}
-KERNELS = ["norm", "state_init", "state_update", "forward", "state_update_rr", "combine"]
+KERNELS = ["norm", "state_init", "state_update", "forward", "state_update_rr", "combine", "state_update_col",
+           "state_init_col"]
 
 
 class NRXLibraryError(RuntimeError):

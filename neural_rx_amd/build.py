@@ -18,12 +18,12 @@ LIB = os.path.join(HERE, "lib", "libnrx.so")
 # one translation unit per strip tier / k_forward mode, so that an edit of one schedule recompiles
 # only its own code object; nrx_device.inc / nrx_launch.inc hold the shared device and launch code
 KERNEL_TUS = ["nrx_k_p16.hip", "nrx_k_p16m.hip", "nrx_k_p16s.hip", "nrx_k_p64.hip", "nrx_k_fwd0.hip",
-              "nrx_k_fwd1.hip", "nrx_k_fwd2.hip", "nrx_k_rr.hip", "nrx_dispatch.hip"]
+              "nrx_k_fwd1.hip", "nrx_k_fwd2.hip", "nrx_k_rr.hip", "nrx_k_col.hip", "nrx_dispatch.hip"]
 SOURCES = [os.path.join(CSRC, f) for f in KERNEL_TUS] + [
     os.path.join(CSRC, "nrx_aerial.hip"), os.path.join(CSRC, "nrx_synth.hip"), os.path.join(CSRC, "nrx_api.cpp")]
 HEADERS = [os.path.join(CSRC, "nrx_internal.h"), os.path.join(HERE, "..", "include", "nrx.h")]
 KERNEL_INCS = [os.path.join(CSRC, "nrx_device.inc"), os.path.join(CSRC, "nrx_launch.inc"),
-               os.path.join(CSRC, "nrx_rr.inc")]
+               os.path.join(CSRC, "nrx_rr.inc"), os.path.join(CSRC, "nrx_col.inc")]
 DEPS = SOURCES + HEADERS + KERNEL_INCS
 ARCH = os.environ.get("NRX_OFFLOAD_ARCH", "gfx950")
 

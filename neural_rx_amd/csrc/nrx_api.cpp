@@ -353,7 +353,7 @@ struct nrx_handle {
   int fused_enabled = 1;    // NRX_FUSED (environment, read once at nrx_create)
   int spin_limit = kFusedSpinLimit;
   int dbg_err = 0;
-  int update_rr = 1;        // nrx_update_schedule (NRX_UPDATE_RR at nrx_create)
+  int update_rr = kSchedDefault;   // nrx_update_schedule (NRX_UPDATE_RR at nrx_create)
   // one-stream rule of the one-launch forward: an event the handle owns, recorded
   // behind every eager one-launch forward, stands for "that forward is done" -- the caller's
   // stream itself is never kept (it may be destroyed between calls).  last_stream is compared,
@@ -497,10 +497,12 @@ int nrx_create(const nrx_desc* desc, const float* const* weights, const int64_t*
   {
     const char* ev = getenv("NRX_UPDATE_RR");   // A/B: 0 = strip update kernels
     if (ev && *ev) {
-      if (ev[0] >= '0' && ev[0] <= '3' && !ev[1]) h->update_rr = ev[0] - '0';
+      char* end = nullptr;
+      const long v = strtol(ev, &end, 10);
+      if (end && !*end && ev[0] >= '0' && ev[0] <= '9' && v >= 0 && v <= kSchedMax) h->update_rr = (int)v;
       else {
         delete h;
-        return fail(NRX_ERR_INVALID_ARG, std::string("NRX_UPDATE_RR must be a stage mask 0..3, got '") + ev + "'");
+        return fail(NRX_ERR_INVALID_ARG, std::string("NRX_UPDATE_RR must be a stage mask 0..31, got '") + ev + "'");
       }
     }
   }
@@ -897,7 +899,8 @@ int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t 
   if (!h) return fail(NRX_ERR_INVALID_ARG, "null argument");
   // every argument < 0 leaves its setting unchanged; spin_limit == 0 restores the
   // default bound
-  if (enable >= 0) h->fused_enabled = enable > 2 ? 2 : enable;
+  if (enable > 2) return fail(NRX_ERR_INVALID_ARG, "enable must be 0 (off), 1 (default) or 2 (force)");
+  if (enable >= 0) h->fused_enabled = enable;
   if (spin_limit >= 0) h->spin_limit = spin_limit > 0 ? spin_limit : kFusedSpinLimit;
   if (inject_err >= 0) h->dbg_err = inject_err;
   return NRX_OK;
@@ -905,7 +908,7 @@ int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t 
 
 int nrx_update_schedule(nrx_handle* h, int32_t update_rr) {
   if (!h) return fail(NRX_ERR_INVALID_ARG, "null argument");
-  if (update_rr > 3) return fail(NRX_ERR_INVALID_ARG, "update_rr is a stage mask 0..3");
+  if (update_rr > kSchedMax) return fail(NRX_ERR_INVALID_ARG, "update_rr is a stage mask 0..31");
   if (update_rr >= 0) h->update_rr = update_rr;
   return NRX_OK;
 }

@@ -47,7 +47,8 @@ hipError_t setup_kernels() {
   (void)cu_count();
   (void)xcc_count();
   const hipError_t es[] = {setup_tier_p16(),     setup_tier_p16m(),    setup_tier_p16s(),   setup_tier_p64(),
-                           setup_kforward_m0(), setup_kforward_m1(), setup_kforward_m2(), setup_update_rr()};
+                           setup_kforward_m0(), setup_kforward_m1(), setup_kforward_m2(), setup_update_rr(),
+                           setup_col()};
   for (hipError_t e : es)
     if (e != hipSuccess) return e;
   return hipSuccess;

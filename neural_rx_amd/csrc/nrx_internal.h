@@ -124,13 +124,23 @@ struct FusedCtl {
   int enabled;   // 0 off, 1 where measured faster (the bench-type schedule), 2 every applicable shape
   int spin_limit;
   int dbg_err;
-  int update_rr;   // three-launch f16 forward: stage mask (1 aggregation, 2 readout) run register-resident
+  int update_rr;   // three-launch f16 forward: stage mask (nrx_update_schedule: 1 / 2 RR aggregation / readout,
+                   // 4 / 8 column aggregation / readout, 16 column StateInit)
 };
+// schedule-mask bits of the three-launch f16 forward (nrx_update_schedule)
+constexpr int kSchedRrAgg = 1, kSchedRrRo = 2, kSchedColAgg = 4, kSchedColRo = 8, kSchedColInit = 16;
+constexpr int kSchedMax = 31;
+// default: the whole-column launches for every stage they apply to, the RR aggregation update
+// where they do not (same-box A/B in profiles/r06/)
+constexpr int kSchedDefault = kSchedColInit | kSchedColAgg | kSchedColRo | kSchedRrAgg;
 constexpr int kFusedSpinLimit = 1 << 21;   // ~0.5 s of s_sleep 4 polls
 
 // Optional per-kernel timing (nrx_profile_enable): events recorded around each launch on
 // the launch stream.  Kernel ids:
-enum KernelId { K_NORM = 0, K_INIT = 1, K_UPDATE = 2, K_FUSED = 3, K_UPDATE_RR = 4, K_COMBINE = 5, K_COUNT = 6 };
+enum KernelId {
+  K_NORM = 0, K_INIT = 1, K_UPDATE = 2, K_FUSED = 3, K_UPDATE_RR = 4, K_COMBINE = 5, K_UPDATE_COL = 6, K_INIT_COL = 7,
+  K_COUNT = 8
+};
 
 struct Prof {
   virtual void begin(int kid, void* stream) = 0;

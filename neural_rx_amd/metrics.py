@@ -37,6 +37,8 @@ def launch_flops_per_re_user(spec: ModelSpec, num_it: int) -> dict:
            "state_update": k["state_update"] + ((num_it - 1) * k["aggregate"] + k["readout"]) / num_it,
            "forward": forward_flops_per_re_user(spec, num_it)}
     out["state_update_rr"] = out["state_update"]   # the register-resident update launch: same work
+    out["state_update_col"] = out["state_update"]  # the whole-column update launch: same work
+    out["state_init_col"] = out["state_init"]
     out["combine"] = 0   # U > 2: the leave-one-out mean pass (k_combine), byte work
     return out
 

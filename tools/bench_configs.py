@@ -31,6 +31,39 @@ CONFIGS = [
 ]
 
 
+def slot_chunks(B: int, U: int, F: int) -> int:
+    """Sub-forwards an f16 forward of B slots runs as (nrx_api.cpp chunk_slots: the largest chunk
+    whose workspace stays below kGzRange = 1 GiB)."""
+    al = lambda n: (n + 255) // 256 * 256   # noqa: E731
+    ws = lambda b: al(b * 8) + 4 * al(b * U * F * 14 * 56 * 2) + al(U * F * 14 * 56 * 2)   # noqa: E731
+    if ws(B) < (1 << 30):
+        return 1
+    lo, hi = 1, B - 1
+    while lo < hi:
+        mid = (lo + hi + 1) // 2
+        if ws(mid) < (1 << 30):
+            lo = mid
+        else:
+            hi = mid - 1
+    return -(-B // lo)
+
+
+def kernel_rows(prof: dict, kfl: dict, re_users: int, chunks: int, steps: int) -> dict:
+    """Per-kernel launch count, average duration and TFLOP/s.  A launch of a chunked forward
+    processes one slot chunk, so its FLOPs are the per-RE-user work of the launch x the chunk's
+    RE-users (re_users / chunks), never the whole batch's.  kfl["state_update"]
+    is the average update launch (aggregation and readout tails differ by < 10 %)."""
+    out = {}
+    for k, (n, ms) in prof.items():
+        if not n:
+            continue
+        avg_s = ms / n * 1e-3
+        per_launch = kfl.get(k, 0) * re_users / chunks
+        out[k] = {"launches": n, "launches_per_forward": round(n / steps, 2), "avg_us": round(avg_s * 1e6, 2),
+                  "tflops": round(per_launch / avg_s / 1e12, 1) if per_launch else None}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
@@ -38,6 +71,8 @@ def main():
     ap.add_argument("--only", default=None, help="substring of the config tag")
     ap.add_argument("--prewarm-s", type=float, default=0.3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--default-mask", type=int, default=-1,
+                    help="schedule mask restored after the A/B runs (-1: the library default kept)")
     a = ap.parse_args()
     import torch
     from neural_rx_amd import metrics
@@ -54,6 +89,8 @@ def main():
         spec = spec_from_config(cfg, ant)
         wl = W.seeded(spec, seed=3) if seeded else W.load(cfg.label)
         eng = CGNNEngine(spec, wl)
+        if a.default_mask >= 0:
+            eng.update_schedule(a.default_mask)
         p = GenParams.from_config(cfg, num_tx=U, num_prbs=prbs, num_rx_ant=ant, var_mcs=var, seed=5)
         gen = SlotGenerator(p)
         sb = gen(B, ebno_to_no(6.0))
@@ -93,6 +130,8 @@ def main():
         def took_of(prof):
             if prof.get("forward", (0, 0))[0]:
                 return "k_forward"
+            if prof.get("state_update_col", (0, 0))[0] or prof.get("state_init_col", (0, 0))[0]:
+                return "three-launch col"
             return "three-launch rr" if prof.get("state_update_rr", (0, 0))[0] else "three-launch"
 
         eng.profile(True)
@@ -100,24 +139,24 @@ def main():
         default_took = took_of(eng.profile_read())
         eng.profile(False)
         res = {}
-        # three schedules: the one-launch forward (forced), three launches with the register-
-        # resident aggregation updates (the default mask 1, where they apply), three launches with
-        # the strip update kernels
+        # four schedules: the one-launch forward (forced), three launches with the whole-column
+        # launches (mask 29: column StateInit / updates where they apply, the RR aggregation update
+        # elsewhere), with the register-resident aggregation updates (mask 1), with the strip
+        # kernels (mask 0)
         for _ in range(2):
-            for mode, rr in (("force", 1), (False, 1), (False, 0)):   # rr: nrx_update_schedule mask
+            for mode, rr in (("force", 1), (False, 29), (False, 1), (False, 0)):   # rr: schedule mask
                 eng.fused_config(enable=mode)
                 eng.update_schedule(rr)
                 el, prof = measure()
                 took = took_of(prof)
                 if took not in res or el < res[took][0]:
                     res[took] = (el, prof)
-        eng.update_schedule(1)
+        eng.update_schedule(a.default_mask)
+        chunks = slot_chunks(B, U, p.num_subcarriers)
         for took, (el, prof) in res.items():
-            kern = {k: {"launches": n, "avg_us": round(ms / n * 1e3, 2),
-                        "tflops": round(kfl[k] * re_users / (ms / n * 1e-3) / 1e12, 1) if kfl[k] else None}
-                    for k, (n, ms) in prof.items() if n}
+            kern = kernel_rows(prof, kfl, re_users, chunks, a.steps)
             row = {"config": tag, "path": took, "default": took == default_took,
-                   "slots_per_gpu": B, "num_it": num_it,
+                   "slots_per_gpu": B, "slot_chunks": chunks, "num_it": num_it,
                    "ms_per_batch": round(el * 1e3, 4), "slots_per_s_per_gpu": round(B / el, 1),
                    "gflop_per_batch": round(fl / 1e9, 2), "whole_forward_tflops": round(fl / el / 1e12, 1),
                    "frac_f16_mfma_peak": round(fl / el / 1e12 / metrics.PEAK_TFLOPS["f16"], 4), "kernels": kern}

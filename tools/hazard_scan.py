@@ -1,7 +1,9 @@
 """Scan gfx950 assembly for the two inline-asm hazards the compiler does not pad (DESIGN.md
-section 10, "Hazards found"): (1) a VALU write of a VGPR followed within 2 instructions by a DPP
-instruction reading it as src0 (needs 2 wait states); (2) the DPP FMAC (inline asm, the
-depthwise) writing a VGPR followed by an MFMA reading it with no wait state in between.  s_nop N
+section 10, "Hazards found"): (1) a VALU write of a VGPR followed by a DPP instruction reading it
+as src0 with fewer than 2 wait states in between; (2) the DPP FMAC (inline asm, the depthwise)
+writing a VGPR followed by an MFMA reading it with fewer than 2 wait states in between (gfx940+:
+LLVM GCNHazardRecognizer's LegacyVALUNotDotWritesVGPRWaitStates = 2).  A hit is a
+pair at distance d <= 2 (d = 1: adjacent, d = 2: one instruction or an s_nop 0 between).  s_nop N
 counts as N + 1 wait states, s_waitcnt as none (measured: an s_waitcnt as the only instruction
 between the two gave wrong MFMA results).  Linear scan per function (labels do not reset the window).
 
@@ -72,9 +74,8 @@ if __name__ == "__main__":
     hits = scan(open(sys.argv[1]).read().splitlines(), want)
     import collections
     kinds = collections.Counter(h[1] for h in hits)
-    for h in hits:
-        if h[1].endswith("d=1"):
-            print(*h, sep=" | ")
+    for h in hits[:40]:
+        print(*h, sep=" | ")
     print(dict(kinds))
-    print(f"{len(hits)} within 2 instructions, {sum(v for k, v in kinds.items() if k.endswith('d=1'))} adjacent")
-    sys.exit(1 if any(h[1].endswith("d=1") for h in hits) else 0)
+    print(f"{len(hits)} with fewer than 2 wait states")
+    sys.exit(1 if hits else 0)
