@@ -24,7 +24,8 @@ SOURCES = [os.path.join(CSRC, f) for f in KERNEL_TUS] + [
 HEADERS = [os.path.join(CSRC, "nrx_internal.h"), os.path.join(HERE, "..", "include", "nrx.h")]
 KERNEL_INCS = [os.path.join(CSRC, "nrx_device.inc"), os.path.join(CSRC, "nrx_launch.inc"),
                os.path.join(CSRC, "nrx_rr.inc"), os.path.join(CSRC, "nrx_col.inc")]
-DEPS = SOURCES + HEADERS + KERNEL_INCS
+# build.py itself: a change of the id rule (source_hash) relinks with a new nrx_build_id
+DEPS = SOURCES + HEADERS + KERNEL_INCS + [os.path.abspath(__file__)]
 ARCH = os.environ.get("NRX_OFFLOAD_ARCH", "gfx950")
 
 
@@ -66,16 +67,51 @@ def _stale(obj: str, src: str) -> bool:
     return open(sig).read() != _sig(src)
 
 
-def source_hash() -> str:
-    """Content hash of every source the library is built from (the kernels, their includes, the
-    host side).  Compiled into the library (nrx_build_id) at every link, so a counter capture
-    (tools/pmc_record.py) and a later bench line can tell whether they describe the same kernels."""
+def strip_comments(text: str) -> str:
+    """C / C++ / HIP source without its comments, whitespace runs collapsed to one space (string
+    and character literals kept verbatim): the code the compiler sees, for source_hash."""
+    out, i, n = [], 0, len(text)
+    while i < n:
+        c = text[i]
+        if c == "/" and i + 1 < n and text[i + 1] == "/":
+            j = text.find("\n", i)
+            i = n if j < 0 else j
+            out.append(" ")
+        elif c == "/" and i + 1 < n and text[i + 1] == "*":
+            j = text.find("*/", i + 2)
+            i = n if j < 0 else j + 2
+            out.append(" ")
+        elif c in "\"'":
+            j = i + 1
+            while j < n and text[j] != c:
+                j += 2 if text[j] == "\\" else 1
+            out.append(text[i:j + 1])
+            i = j + 1
+        else:
+            out.append(c)
+            i += 1
+    return " ".join("".join(out).split())
+
+
+def hash_sources(texts: dict) -> str:
+    """16-hex-digit hash of {file name: source text}, comments and whitespace ignored."""
     h = hashlib.sha256()
-    for p in sorted(set(SOURCES + HEADERS + KERNEL_INCS)):
-        h.update(os.path.basename(p).encode() + b"\0")
-        with open(p, "rb") as f:
-            h.update(f.read())
+    for name in sorted(texts):
+        h.update(name.encode() + b"\0" + strip_comments(texts[name]).encode() + b"\0")
     return h.hexdigest()[:16]
+
+
+def source_hash() -> str:
+    """Hash of the code of every source the library is built from (the kernels, their includes,
+    the host side) -- comments and whitespace excluded, so a comment-only edit keeps the id
+    (VERDICT r05 item 5).  Compiled into the library (nrx_build_id) at every link, so a counter
+    capture (tools/pmc_record.py) and a later bench line can tell whether they describe the same
+    kernels."""
+    texts = {}
+    for p in sorted(set(SOURCES + HEADERS + KERNEL_INCS)):
+        with open(p, encoding="utf-8") as f:
+            texts[os.path.basename(p)] = f.read()
+    return hash_sources(texts)
 
 
 def _build_id_object(verbose: bool, obj_dir: str = OBJ_DIR, tag: str = "") -> str:
