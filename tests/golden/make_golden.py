@@ -13,9 +13,10 @@ exercised:
 
 The trained nrx_rt weights (Keras Dense kernels ``[in, out]``) are loaded into the
 ``nn.Linear`` layers transposed.  Output: ``tests/golden/ref_modules_nrx_rt.npz``
-(inputs and outputs only -- data, no reference code).
+(inputs and outputs only -- data, no reference code), and ``tests/golden/ref_sepconv_nrx_rt.npz``
+from the reference's ``SeparableConv2d`` (sepconv_golden).
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [--sepconv]
 """
 from __future__ import annotations
 
@@ -47,6 +48,55 @@ def _placeholder_modules():
     for name, mod in [("sionna", sionna), ("sionna.utils", utils), ("sionna.ofdm", ofdm),
                       ("sionna.nr", nr), ("tensorflow", tf)]:
         sys.modules.setdefault(name, mod)
+
+
+REF_PT = "/root/reference/utils/neural_rx copy_pytorch.py"
+
+
+def reference_separable_conv2d():
+    """The reference's torch ``SeparableConv2d`` (``utils/neural_rx copy_pytorch.py:34-51``: a
+    depthwise ``nn.Conv2d(groups=in_channels, padding=kernel_size // 2)`` then a 1x1 pointwise
+    conv).  The file keeps it commented out, so its comment markers are stripped in memory and the
+    class is executed from the reference text; nothing of it is written to the repository."""
+    import torch
+    import torch.nn as nn
+    lines = open(REF_PT).read().splitlines()
+    start = next(i for i, ln in enumerate(lines) if ln.startswith("# class SeparableConv2d"))
+    end = next(i for i in range(start + 1, len(lines)) if lines[i].startswith("# def "))
+    src = "\n".join(ln[2:] if ln.startswith("# ") else ln.lstrip("#") for ln in lines[start:end])
+    ns = {"nn": nn, "torch": torch}
+    exec(compile(src, REF_PT, "exec"), ns)
+    return ns["SeparableConv2d"]
+
+
+def sepconv_golden():
+    """Every trained StateInit and UpdateState (iteration 0) separable layer of nrx_rt run through
+    the reference's SeparableConv2d (Keras depthwise [3, 3, C, 1] -> torch [C, 1, 3, 3], pointwise
+    [1, 1, C, O] -> [O, C, 1, 1]; the reference class has bias=False, the Keras pointwise bias is
+    added to its output) on small random NCHW inputs -> tests/golden/ref_sepconv_nrx_rt.npz."""
+    import torch
+    from neural_rx_amd import weights as W
+    from neural_rx_amd.config import get_config, spec_from_config
+    from oracle import cgnn_ref
+    SeparableConv2d = reference_separable_conv2d()
+    spec = spec_from_config(get_config("nrx_rt"))
+    cw = cgnn_ref.split_keras_weights(W.load("nrx_rt"), spec)
+    rng = np.random.default_rng(20261018)
+    out = {}
+    layers = [("init", k, w) for k, w in enumerate(cw.init[0])] + [("upd", k, w) for k, w in enumerate(cw.update[0])]
+    for name, k, w in layers:
+        cin, cout = w.pw.shape[2], w.pw.shape[3]
+        m = SeparableConv2d(cin, cout, 3)
+        with torch.no_grad():
+            m.depthwise.weight.copy_(torch.from_numpy(np.transpose(w.dw, (2, 3, 0, 1)).copy()))
+            m.pointwise.weight.copy_(torch.from_numpy(np.transpose(w.pw, (3, 2, 0, 1)).copy()))
+            x = (rng.standard_normal((1, cin, 6, 14)) * 2).astype(np.float32)   # N, C, F, T
+            y = m(torch.from_numpy(x)).numpy() + w.b.astype(np.float32)[None, :, None, None]
+        out[f"{name}{k}_x"] = x
+        out[f"{name}{k}_y"] = y
+    path = os.path.join(HERE, "ref_sepconv_nrx_rt.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", os.path.relpath(path, ROOT), {k: v.shape for k, v in out.items()})
 
 
 def main():
@@ -112,4 +162,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--sepconv" in sys.argv:
+        sepconv_golden()
+    else:
+        main()
+        sepconv_golden()
