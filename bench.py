@@ -256,14 +256,15 @@ def main():
             kern[name] = {"launches": n, "avg_us": round(avg_s * 1e6, 3),
                           "avg_us_event_pairs": round(ms / n * 1e3, 3),
                           "tflops": round(fl / avg_s / 1e12, 2) if fl else None}
-    fused = prof.get("forward", (0, 0.0))[0] > 0
+    fused_name = "forward_col" if prof.get("forward_col", (0, 0.0))[0] > 0 else "forward"
+    fused = prof.get(fused_name, (0, 0.0))[0] > 0
     # the dominant kernel: the one-launch forward when the engine took it (throughput tier),
     # else the state-update launches of the three-launch forward, whichever kernel ran each
     # stage (nrx_update_schedule: the RR launch for the aggregation updates and the strip
     # k_update for the readout update by default) -- averaged over all update launches, as
     # kflops["state_update"] is the average work of one update launch
     if fused:
-        dom, upd = "forward", ["forward"]
+        dom, upd = fused_name, [fused_name]
     else:
         upd = [k for k in ("state_update_col", "state_update_rr", "state_update") if prof.get(k, (0, 0.0))[0]]
         dom = "state_update"
@@ -280,8 +281,10 @@ def main():
     compulsory = metrics.compulsory_bytes_per_forward(spec, B, U, F, with_h=True)
     if fused:
         alg_bytes = metrics.forward_bytes_per_re_user(spec, num_it, U, elem) * re_users
-        pmc_field, kname = "k_forward_bytes_per_launch", \
-            "k_forward (StateInit + num_it state updates + readouts: one persistent launch)"
+        pmc_field, kname = "k_forward_bytes_per_launch", (
+            "k_fwd_col (StateInit + num_it state updates + readouts as column items: one persistent launch)"
+            if fused_name == "forward_col" else
+            "k_forward (StateInit + num_it state updates + readouts: one persistent launch)")
         mixed = metrics.forward_mixed_bound_tflops(spec, num_it, peak) if args.precision == "f16" else None
         mixed_note = ("the forward's depthwise FLOPs at the VALU peak (157 TF) + its dense FLOPs at the "
                       "f16 MFMA peak, pipes overlapped (metrics.forward_mixed_bound_tflops)")
@@ -314,7 +317,8 @@ def main():
     sq_path = os.path.join(ROOT, "profiles", "pmc_sq.json")
     if os.path.exists(sq_path):
         try:
-            sq = json.load(open(sq_path)).get(key, {}).get("k_forward" if fused else "k_update", {})
+            sq = json.load(open(sq_path)).get(key, {}).get(
+                ("k_fwd_col" if fused_name == "forward_col" else "k_forward") if fused else "k_update", {})
         except Exception:
             sq = {}
     # counters are quoted only from a capture of the library that is running:
@@ -363,7 +367,8 @@ def main():
                 "counters_build_id": sq.get("build_id"),
                 "counters_match_build": match}
     if fused:
-        upd_items = args.steps * num_it * U * B * ((F + 23) // 24)
+        upd_items = args.steps * num_it * U * B * (((F + 23) // 24) if fused_name == "forward" else
+                                                   (1 if F <= 48 else (F + 43) // 44))
         roofline["fused_queue"] = {"update_items_waited": fused_st["waited"], "update_items": upd_items,
                                    "polls": fused_st["polls"], "error": fused_st["error"],
                                    "ok": fused_st["waited"] == 0 and fused_st["error"] == 0,

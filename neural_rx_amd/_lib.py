@@ -34,7 +34,7 @@ EXPORTS = [
 # enum nrx_y_layout
 Y_LAYOUTS = {"cgnn": 0, "sionna": 1, "split": 2}
 KERNELS = ["norm", "state_init", "state_update", "forward", "state_update_rr", "combine", "state_update_col",
-           "state_init_col"]
+           "state_init_col", "forward_col"]
 
 
 class NRXLibraryError(RuntimeError):

@@ -13,13 +13,16 @@ hipError_t launch_forward_f16(const FwdArgs<_Float16, float, _Float16>& args,
     if (small_strips_fit<P16S>(args)) return run_tier_p16s(args, W, num_it, st, prof);
     if (small_strips_fit<P16M>(args)) return run_tier_p16m(args, W, num_it, st, prof);
   }
+  if (fwd_col_applicable(args, num_it, fc)) return launch_fwd_col(args, W, num_it, st, prof, fc);
   if (fused_applicable<P16>(args, num_it, fc)) return run_fused<P16>(args, W, num_it, st, prof, fc);
   return run_tier_p16(args, W, num_it, st, prof, fc.update_rr);
 }
 
+// whether a forward takes a one-launch path (k_fwd_col or k_forward: the handle's counters, one
+// stream at a time)
 bool fused_would_run(const FwdArgs<_Float16, float, _Float16>& args, int num_it, const FusedCtl& fc) {
   if (NRX_SMALL_STRIPS != 0 && (small_strips_fit<P16S>(args) || small_strips_fit<P16M>(args))) return false;
-  return fused_applicable<P16>(args, num_it, fc);
+  return fwd_col_applicable(args, num_it, fc) || fused_applicable<P16>(args, num_it, fc);
 }
 
 size_t fused_sync_bytes() { return kFusedSyncBytes; }

@@ -129,7 +129,8 @@ struct FusedCtl {
 };
 // schedule-mask bits of the three-launch f16 forward (nrx_update_schedule)
 constexpr int kSchedRrAgg = 1, kSchedRrRo = 2, kSchedColAgg = 4, kSchedColRo = 8, kSchedColInit = 16;
-constexpr int kSchedMax = 31;
+constexpr int kSchedColFwd = 32;   // the one-launch column forward (k_fwd_col) where it applies
+constexpr int kSchedMax = 63;
 // default: the whole-column launches for every stage they apply to, the RR aggregation update
 // where they do not (same-box A/B in profiles/r06/)
 constexpr int kSchedDefault = kSchedColInit | kSchedColAgg | kSchedColRo | kSchedRrAgg;
@@ -139,7 +140,7 @@ constexpr int kFusedSpinLimit = 1 << 21;   // ~0.5 s of s_sleep 4 polls
 // the launch stream.  Kernel ids:
 enum KernelId {
   K_NORM = 0, K_INIT = 1, K_UPDATE = 2, K_FUSED = 3, K_UPDATE_RR = 4, K_COMBINE = 5, K_UPDATE_COL = 6, K_INIT_COL = 7,
-  K_COUNT = 8
+  K_FWD_COL = 8, K_COUNT = 9
 };
 
 struct Prof {

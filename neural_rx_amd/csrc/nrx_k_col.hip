@@ -68,6 +68,77 @@ hipError_t launch_update_col(const BlockParams<P16>& bp0, bool last, hipStream_t
   return hipGetLastError();
 }
 
+// the one-launch column forward (k_fwd_col): U <= 2 (no combine stage), one StateInit over 2A = 8,
+// GZ conv1 (workspace below 1 GB), one LLR head whose readout fits, at most one item per CU and
+// stage (every item stages its weights), a device whose XCDs hold equal CU counts
+bool fwd_col_applicable(const FwdArgs<_Float16, float, _Float16>& a, int num_it, const FusedCtl& fc) {
+  // fc.enabled == 0 (NRX_FUSED=0, nrx_fused_config(h, 0, ..)): no one-launch forward of any kind
+  if (!fc.sync || !fc.enabled || !(fc.update_rr & kSchedColFwd)) return false;
+  const int cus = cu_count(), nx = xcc_count();
+  if (nx < 1 || nx > 8 || cus % nx != 0) return false;
+  const long items = (long)a.B * a.U * col_strips(a.F);
+  return a.U <= kInlineUsers && col_init_applicable(a) && a.ws_bytes < kGzOob && a.pe16 && a.H == 1 &&
+         rr_heads_fit(a.bits_max, 16, 2 * a.A) && items <= cus && num_it >= 1 && 1 + num_it <= kColMaxStages &&
+         a.B <= kFusedMaxB;
+}
+
+hipError_t launch_fwd_col(const FwdArgs<_Float16, float, _Float16>& args, const ModelW<_Float16, float>& W, int num_it,
+                          hipStream_t st, Prof* prof, const FusedCtl& fc) {
+  auto B_ = [&](int kid) { if (prof) prof->begin(kid, st); };
+  auto E_ = [&](int kid) { if (prof) prof->end(kid, st); };
+  ColFwdParams fp{};
+  fp.sync = reinterpret_cast<FusedSync*>(fc.sync);
+  fp.nst = 1 + num_it;
+  fp.nq = xcc_count();
+  fp.spin_limit = fc.spin_limit;
+  fp.dbg_err = fc.dbg_err;
+  const int nq = args.F * kT * 2 * args.A / 4;
+  const bool norm_pre = nq > kNormFusedMaxQ;
+  if (norm_pre) {
+    B_(K_NORM);
+    k_norm<<<args.B, 1024, 0, st>>>(args.y, nq, args.norm);
+    E_(K_NORM);
+  }
+  FwdArgs<_Float16, float, _Float16> a = args;
+  for (int s = 0; s < fp.nst; ++s) {
+    BlockParams<P16>& bp = fp.st[s];
+    bp.inline_combine = 1;
+    bp.pair = 0;
+    bp.order_rev = 0;
+    bp.norm_pre = norm_pre;
+    bp.strips = col_strips(args.F);
+    bp.m = 0;
+    bp.gz = 1;
+    bp.llr[0][0] = W.llr[0][0];
+    bp.llr[0][1] = W.llr[0][1];
+    bp.chest[0] = W.chest[0];
+    bp.chest[1] = W.chest[1];
+    if (s == 0) {
+      for (int l = 0; l < 3; ++l) bp.w[l] = W.init[0][l];
+      bp.tail = TAIL_AGG;
+      bp.agg[0] = W.agg[0][0];
+      bp.agg[1] = W.agg[0][1];
+    } else {
+      std::swap(a.s_in, a.s_out);
+      std::swap(a.a, a.a_out);
+      const int i = s - 1;
+      for (int l = 0; l < 3; ++l) bp.w[l] = W.upd[i][l];
+      const bool last = i == num_it - 1;
+      bp.tail = last ? TAIL_READOUT_WB : TAIL_AGG;
+      if (!last) {
+        bp.agg[0] = W.agg[i + 1][0];
+        bp.agg[1] = W.agg[i + 1][1];
+      }
+    }
+    bp.a = a;
+  }
+  col_stamp_select(st);
+  B_(K_FWD_COL);
+  k_fwd_col<16><<<cu_count(), 512, kColLds, st>>>(fp);
+  E_(K_FWD_COL);
+  return hipGetLastError();
+}
+
 hipError_t setup_col() {
   hipError_t e = hipSuccess;
   auto set = [&](const void* f) {
@@ -79,6 +150,7 @@ hipError_t setup_col() {
   set((const void*)k_update_col<32, TAIL_AGG>);
   set((const void*)k_update_col<16, TAIL_READOUT_WB>);
   set((const void*)k_update_col<32, TAIL_READOUT_WB>);
+  set((const void*)k_fwd_col<16>);
   return e;
 }
 

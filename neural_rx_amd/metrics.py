@@ -39,6 +39,7 @@ def launch_flops_per_re_user(spec: ModelSpec, num_it: int) -> dict:
     out["state_update_rr"] = out["state_update"]   # the register-resident update launch: same work
     out["state_update_col"] = out["state_update"]  # the whole-column update launch: same work
     out["state_init_col"] = out["state_init"]
+    out["forward_col"] = out["forward"]            # the one-launch column forward
     out["combine"] = 0   # U > 2: the leave-one-out mean pass (k_combine), byte work
     return out
 

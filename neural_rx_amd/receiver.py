@@ -132,9 +132,10 @@ class CGNNEngine:
         """Stage schedule of the three-launch f16 forward (include/nrx.h nrx_update_schedule): a
         mask -- bits 0 / 1 run the aggregation / readout update stages as the register-resident
         16-row launch (k_update_rr), bits 2 / 3 as the whole-column launch (k_update_col, taken
-        over the RR bit), bit 4 runs StateInit as k_init_col -- each where it applies (the strip
-        kernels elsewhere; outputs are bit-identical either way); True = 3, False = 0 (strip
-        kernels everywhere), None = unchanged."""
+        over the RR bit), bit 4 runs StateInit as k_init_col, bit 5 the whole forward as the
+        one-launch column forward k_fwd_col -- each where it applies (the strip kernels elsewhere;
+        outputs are bit-identical either way); True = 3, False = 0 (strip kernels everywhere),
+        None = unchanged."""
         m = -1 if rr is None else 3 if rr is True else 0 if rr is False else int(rr)
         _lib.check(self._lib.nrx_update_schedule(self._h, m))
 

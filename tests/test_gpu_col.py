@@ -127,3 +127,72 @@ def test_col_users_combine_pass(users):
     case = make_case("nrx_rt", batch=64, users=users, prbs=4, snr_db=12, seed=80 + users,
                      active=np.random.default_rng(80 + users).integers(0, 2, size=(64, users)).astype(np.float32))
     _check(case, oracle=users == 3)
+
+
+# ---------------------------------------------------------------- one-launch column forward
+FWD = COL | 32
+
+
+def _run_fwd(case, mask=FWD):
+    eng = _engine(case)
+    eng.fused_config(enable=True)
+    eng.update_schedule(mask)
+    eng.profile(True)
+    out = run_engine(case, "f16", eng)
+    prof = eng.profile_read()
+    eng.profile(False)
+    eng.check()          # no dependency-wait timeout, every counter complete
+    return out, prof
+
+
+def _check_fwd(case, oracle=True):
+    ref, _ = _run(case, 0)
+    got, pg = _run_fwd(case)
+    assert pg["forward_col"][0] == 1 and pg["state_update"][0] == 0 and pg["forward"][0] == 0, pg
+    assert np.array_equal(ref["llr_raw"], got["llr_raw"]), np.abs(ref["llr_raw"] - got["llr_raw"]).max()
+    assert np.array_equal(ref["h_hat"], got["h_hat"])
+    if oracle:
+        c = compare(run_oracle(case), got)
+        assert c["llr_rel"] < 0.10 and c["llr_rms_rel"] < 0.02 and c["flip_rate_confident"] <= 1e-3, c
+
+
+def test_fwd_col_bench_shape():
+    # BASELINE configs[1] as ONE launch (k_fwd_col): StateInit, aggregation and readout items behind
+    # per-slot counters, bit-identical to the three strip launches
+    _check_fwd(make_case("nrx_rt", batch=128, users=2, prbs=4, snr_db=12, seed=91))
+
+
+def test_fwd_col_repeated_and_inactive_users():
+    # the counters are reset by the last workgroup: consecutive forwards on one handle agree; random
+    # activity, fewer items than CUs
+    case = make_case("nrx_rt", batch=96, users=2, prbs=4, snr_db=12, seed=92,
+                     active=np.random.default_rng(92).integers(0, 2, size=(96, 2)).astype(np.float32))
+    ref, _ = _run(case, 0)
+    for _ in range(3):
+        got, pg = _run_fwd(case)
+        assert pg["forward_col"][0] == 1
+        assert np.array_equal(ref["llr_raw"], got["llr_raw"])
+
+
+def test_fwd_col_u1_two_prb():
+    # U = 1 (ips = 1), F = 24 (positions 24..47 past the grid); 200 slots <= 256 CUs (and too many
+    # items for the small-strip latency tiers, which take precedence)
+    _check_fwd(make_case("nrx_rt", batch=200, users=1, prbs=2, snr_db=12, seed=93))
+
+
+def test_fwd_col_masking_8_iterations():
+    # nrx_large_var_mcs_64qam_masking (BASELINE cfg4'): one StateInit, 8 iterations (9 stages), one
+    # 6-bit head; 128 slots x 2 users = 256 items per stage
+    case = make_case("nrx_large_var_mcs_64qam_masking", batch=128, users=2, prbs=4, snr_db=14, seed=94)
+    ref, _ = _run(case, 0)
+    got, pg = _run_fwd(case)
+    assert pg["forward_col"][0] == 1, pg
+    assert np.array_equal(ref["llr_raw"], got["llr_raw"])
+    assert np.array_equal(ref["h_hat"], got["h_hat"])
+
+
+def test_fwd_col_not_taken_beyond_one_item_per_cu():
+    # 256 slots x 2 users > CUs: the three column launches run instead
+    case = make_case("nrx_rt", batch=256, users=2, prbs=4, snr_db=12, seed=95)
+    _, pg = _run_fwd(case)
+    assert pg["forward_col"][0] == 0 and pg["state_update_col"][0] == 2, pg

@@ -199,7 +199,9 @@ def test_fused_second_stream_refused_while_busy():
     args = _device_args(case)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     with torch.cuda.stream(s1):
-        torch.cuda._sleep(50_000_000)             # the forward queued behind a spin kernel
+        # the forward queued behind a spin kernel (~0.1 s: the second call's host work -- output
+        # and workspace allocations on a stream new to the caching allocator -- must fit inside it)
+        torch.cuda._sleep(200_000_000)
         eng.forward(*args, num_it=None, precision="f16")
     with torch.cuda.stream(s2):
         with pytest.raises(NRXError) as ei:

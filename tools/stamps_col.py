@@ -21,7 +21,7 @@ import torch  # noqa: E402
 
 from neural_rx_amd import _lib  # noqa: E402
 
-path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(_lib.LIB_PATH), "diag", "libnrx.so")
+path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(_lib.LIB_PATH), "diag", "stamps", "libnrx.so")
 lib = _lib.load(path)
 lib.nrx_debug_col_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 from neural_rx_amd import synth, weights as W  # noqa: E402
@@ -34,7 +34,8 @@ spec = spec_from_config(cfg)
 groups = tuple(i % 2 for i in range(U))
 sl = synth.generate(B, U, prbs, 4, [4] * U, groups, snr_db=10, seed=3)
 eng = CGNNEngine(spec, W.load("nrx_rt"))
-eng.fused_config(enable=False)
+# mask bit 32 = the one-launch column forward (k_fwd_col), which needs the one-launch paths on
+eng.fused_config(enable=bool(int(os.environ["NRX_UPDATE_RR"]) & 32))
 t = lambda a: torch.from_numpy(a).cuda()
 pe = t(compute_pe(U, 12 * prbs, (2, 11), groups))
 dy, dh, da = t(sl.y), t(sl.h_hat), t(sl.active)
@@ -58,6 +59,14 @@ for k in range(4):
     print(f"item {k}: {ok.sum()} workgroups, item {tot.mean():.0f} cycles (wave 0), min {tot.min()} max {tot.max()}")
     for w in (0, 1):
         print("   wave", 4 * w, "  ".join(f"{nm} {(st[ok, k, b, w] - st[ok, k, a, w]).mean():6.0f}" for nm, a, b in phases))
+for k in range(3):   # the one-launch forward: gap between a workgroup's consecutive items
+    ok = (st[:, k, 6, 0] != 0) & (st[:, k + 1, 0, 0] != 0)
+    if ok.any():
+        gap = st[ok, k + 1, 0, 0] - st[ok, k, 6, 0]
+        w = st[ok, k + 1, 7, 1]   # after the dependency wait (k_fwd_col diagnostic stamp)
+        part = f"; to the wait's end {(w - st[ok, k, 6, 0]).mean():.0f}, then {(st[ok, k + 1, 0, 0] - w).mean():.0f}" \
+            if (w != 0).all() else ""
+        print(f"gap item {k} -> {k + 1} (signal, dequeue, dependency wait): mean {gap.mean():.0f} max {gap.max()} cycles{part}")
 stage = st[:, 0, 0, 0] - st[:, 0, 7, 0]
 ok = (st[:, 0, 7, 0] != 0) & (st[:, 0, 0, 0] != 0)
 if ok.any():
