@@ -502,7 +502,7 @@ int nrx_create(const nrx_desc* desc, const float* const* weights, const int64_t*
       if (end && !*end && ev[0] >= '0' && ev[0] <= '9' && v >= 0 && v <= kSchedMax) h->update_rr = (int)v;
       else {
         delete h;
-        return fail(NRX_ERR_INVALID_ARG, std::string("NRX_UPDATE_RR must be a stage mask 0..63, got '") + ev + "'");
+        return fail(NRX_ERR_INVALID_ARG, std::string("NRX_UPDATE_RR must be a stage mask 0..127, got '") + ev + "'");
       }
     }
   }
@@ -908,7 +908,7 @@ int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t 
 
 int nrx_update_schedule(nrx_handle* h, int32_t update_rr) {
   if (!h) return fail(NRX_ERR_INVALID_ARG, "null argument");
-  if (update_rr > kSchedMax) return fail(NRX_ERR_INVALID_ARG, "update_rr is a stage mask 0..63");
+  if (update_rr > kSchedMax) return fail(NRX_ERR_INVALID_ARG, "update_rr is a stage mask 0..127");
   if (update_rr >= 0) h->update_rr = update_rr;
   return NRX_OK;
 }

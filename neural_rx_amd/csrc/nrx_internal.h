@@ -130,7 +130,10 @@ struct FusedCtl {
 // schedule-mask bits of the three-launch f16 forward (nrx_update_schedule)
 constexpr int kSchedRrAgg = 1, kSchedRrRo = 2, kSchedColAgg = 4, kSchedColRo = 8, kSchedColInit = 16;
 constexpr int kSchedColFwd = 32;   // the one-launch column forward (k_fwd_col) where it applies
-constexpr int kSchedMax = 63;
+// bits 2 / 3 on grids wider than one 48-position column too (44-output strips with a halo; by
+// default those grids keep the RR / strip updates, measured faster there: profiles/r06/configs)
+constexpr int kSchedColWide = 64;
+constexpr int kSchedMax = 127;
 // default: the whole-column launches for every stage they apply to, the RR aggregation update
 // where they do not (same-box A/B in profiles/r06/)
 constexpr int kSchedDefault = kSchedColInit | kSchedColAgg | kSchedColRo | kSchedRrAgg;

@@ -14,11 +14,13 @@ bool col_init_applicable(const FwdArgs<_Float16, float, _Float16>& a) {
   return a.num_init == 1 && 2 * a.A == 8 && a.init_cinp == 32;
 }
 
-bool update_col_applicable(const FwdArgs<_Float16, float, _Float16>& a, bool gz, bool last) {
+bool update_col_applicable(const FwdArgs<_Float16, float, _Float16>& a, bool gz, bool last, int sched) {
   // conv1 reads [a | s | pe] from memory (GZ): a = the other user's act*sp plane (U = 2), none
-  // (U = 1) or the a_u plane the combine pass wrote (U > 2)
+  // (U = 1) or the a_u plane the combine pass wrote (U > 2); a grid wider than one column only
+  // with kSchedColWide (44-output strips measured slower than the RR launch at cfg3 / cfg5)
   const int chp = 2 * a.A <= 16 ? 16 : 32;
   if (!gz || 2 * a.A > 32) return false;
+  if (col_strips(a.F) > 1 && !(sched & kSchedColWide)) return false;
   return !last || (a.H == 1 && rr_heads_fit(a.bits_max, chp, 2 * a.A));
 }
 

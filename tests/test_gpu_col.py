@@ -14,6 +14,7 @@ from tests.helpers import compare, make_case, run_engine, run_oracle
 pytestmark = pytest.mark.gpu
 
 COL = 4 | 8 | 16
+WIDE = COL | 64      # column updates on grids wider than 48 subcarriers too (off by default)
 _ENGINES = {}
 
 
@@ -71,7 +72,7 @@ def test_col_u1_two_strips_random_activity():
     # strip's rows 16..47 past the grid; inactive slots
     case = make_case("nrx_rt", batch=96, users=1, prbs=5, snr_db=10, seed=73,
                      active=np.random.default_rng(73).integers(0, 2, size=(96, 1)).astype(np.float32))
-    _check(case)
+    _check(case, mask=WIDE)
 
 
 def test_col_u2_inactive_user():
@@ -89,14 +90,14 @@ def test_col_several_items_per_workgroup():
     # F = 96: three strips, 768 items on 256 CUs -- the readout launch restages its conv1 / conv2
     # images after every item (the heads sit over them), the StateInit / aggregation launches loop
     case = make_case("nrx_rt", batch=128, users=2, prbs=8, snr_db=12, seed=76)
-    _check(case)
+    _check(case, mask=WIDE)
 
 
 def test_col_large_grid_norm_pass():
     # 273 PRB (F = 3276 > kNormFusedMaxQ float4s per slot): the slot norm comes from the k_norm
     # pass; 75 strips, more items than CUs
     case = make_case("nrx_rt", batch=2, users=2, prbs=273, snr_db=12, seed=77)
-    _check(case, oracle=False)
+    _check(case, oracle=False, mask=WIDE)
 
 
 def test_col_16_antennas_8_iterations():
@@ -104,7 +105,17 @@ def test_col_16_antennas_8_iterations():
     # stage runs the column launch; nrx_large topology (8 iterations), seeded weights, 132 PRB
     case = make_case("nrx_large", batch=4, users=2, prbs=132, num_rx_ant=16, seeded_weights=True,
                      random_inputs=True, seed=78)
-    _check(case, oracle=False, init_col=False)
+    _check(case, oracle=False, init_col=False, mask=WIDE)
+
+
+def test_col_wide_grid_default_keeps_rr():
+    # by default a grid wider than one column runs the column StateInit and the RR aggregation /
+    # strip readout updates (measured faster there: DESIGN.md section 4)
+    case = make_case("nrx_rt", batch=64, users=2, prbs=8, snr_db=12, seed=70)
+    ref, _ = _run(case, 0)
+    got, pg = _run(case, 29)
+    assert pg["state_update_col"][0] == 0 and pg["state_update_rr"][0] == 1 and pg["state_init_col"][0] == 1, pg
+    assert np.array_equal(ref["llr_raw"], got["llr_raw"])
 
 
 def test_col_var_io():

@@ -124,24 +124,24 @@ def test_rr_users_4_8_combine_pass(users):
 
 
 def test_update_schedule_mask_validation(monkeypatch):
-    # nrx_update_schedule takes a stage mask 0..63 (< 0: unchanged); NRX_UPDATE_RR must be a
-    # decimal 0..63 or nrx_create fails (no silent fallback to a schedule the caller did not ask for)
+    # nrx_update_schedule takes a stage mask 0..127 (< 0: unchanged); NRX_UPDATE_RR must be a
+    # decimal 0..127 or nrx_create fails (no silent fallback to a schedule the caller did not ask for)
     from neural_rx_amd import _lib
     from neural_rx_amd.receiver import CGNNEngine
     case = make_case("nrx_rt", batch=2, users=2, prbs=4, seed=63)
     eng = CGNNEngine(case.spec, case.weights)
     try:
-        for m in (0, 1, 2, 3, 4, 16, 29, 31, 61, 63, -1, True, False, None):
+        for m in (0, 1, 2, 3, 4, 16, 29, 31, 61, 63, 64, 127, -1, True, False, None):
             eng.update_schedule(m)
         with pytest.raises(_lib.NRXError):
-            eng.update_schedule(64)
+            eng.update_schedule(128)
         # nrx_fused_config: enable 0 / 1 / 2 (< 0 unchanged); 3 is an error, not "force" 
         assert eng._lib.nrx_fused_config(eng._h, 3, -1, -1) == _lib.NRX_ERR_INVALID_ARG
         assert eng._lib.nrx_fused_config(eng._h, 2, -1, -1) == 0
         assert eng._lib.nrx_fused_config(eng._h, 1, -1, -1) == 0
     finally:
         eng.close()
-    for bad in ("64", "on", "1x", "-1"):
+    for bad in ("128", "on", "1x", "-1"):
         monkeypatch.setenv("NRX_UPDATE_RR", bad)
         with pytest.raises(_lib.NRXError):
             CGNNEngine(case.spec, case.weights)

@@ -79,9 +79,9 @@ def running_build_id():
 def main(key, source, dirs, cus=256):
     build_id = running_build_id()
     pk = per_dispatch(dirs)
-    fwd = {k: v for k, v in pk.items() if k.startswith("nrx::k_forward")}
+    fwd = {k: v for k, v in pk.items() if k.startswith("nrx::k_forward") or k.startswith("nrx::k_fwd_col")}
     name, c = next(iter(fwd.items())) if fwd else (None, {})
-    sq_key = "k_forward"
+    sq_key = "k_fwd_col" if name and name.startswith("nrx::k_fwd_col") else "k_forward"
     if not fwd:
         # three-launch forward: the dominant kernel is k_update (its instantiations pooled,
         # per-dispatch means weighted by their dispatch counts)
@@ -93,6 +93,19 @@ def main(key, source, dirs, cus=256):
             c = {ck: sum(v.get(ck, 0.0) * cnt.get(k, 0) for k, v in ups.items()) / n for ck in keys}
             name, sq_key = "nrx::k_update (all instantiations)", "k_update"
     traffic, sq = {}, {}
+
+    def sq_fracs(cs):
+        life = 4 * cs["SQ_WAVE_CYCLES"] / cs["SQ_WAVES"]
+        simds = 4 * cus
+        r = {"wave_lifetime_cycles": round(life)}
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in cs:
+            r["mfma_busy_frac"] = round(cs["SQ_VALU_MFMA_BUSY_CYCLES"] / simds / life, 4)
+        if "SQ_INSTS_VALU" in cs:
+            r["valu_issue_frac"] = round(cs["SQ_INSTS_VALU"] * VALU_ISSUE_CYCLES / simds / life, 4)
+        if "SQ_WAIT_ANY" in cs:
+            r["wait_frac"] = round(cs["SQ_WAIT_ANY"] / cs["SQ_WAVE_CYCLES"], 4)
+        r["counters"] = {k: round(v, 1) for k, v in sorted(cs.items())}
+        return r
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         fb, wb = 2 * c["FETCH_SIZE"] * 1024, c["WRITE_SIZE"] * 1024
         traffic = {"k_forward_bytes_per_launch": round(fb + wb), "source": source, "build_id": build_id,
@@ -111,6 +124,10 @@ def main(key, source, dirs, cus=256):
             rec["wait_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
         rec["counters"] = {k: round(v, 1) for k, v in sorted(c.items())}
         sq = {sq_key: rec}
+        # every kernel of the forward on its own (StateInit included: VERDICT r05 item 1)
+        sq["per_kernel"] = {"source": source, "build_id": build_id,
+                            **{k: sq_fracs(cs) for k, cs in pk.items()
+                               if k.startswith("nrx::") and "SQ_WAVE_CYCLES" in cs and cs.get("SQ_WAVES")}}
     if not fwd:
         # three-launch forward (e.g. cfg5's per-GPU shard, U = 8): every kernel's bytes per
         # dispatch, and the forward's total = sum over kernels of mean x dispatches per forward
