@@ -54,7 +54,8 @@ def test_cfg4_var_io():
     case = make_case("nrx_rt_var_mcs", batch=128, users=2, prbs=4, random_inputs=True, seed=4,
                      mcs_choice=rng.integers(0, 2, size=(128, 2)))
     prof = _profile(case)
-    assert prof == {"state_init": 2, "state_update_col": 1, "state_update": 1}, prof
+    # (the profiler times the StateInit stage's two launches as one event pair)
+    assert prof == {"state_init": 1, "state_update_col": 1, "state_update": 1}, prof
 
 
 def test_cfg4p_masking_8_iterations():
