@@ -317,14 +317,15 @@ int nrx_profile_read(nrx_handle* h, int32_t kernel, int64_t* launches, double* t
  * fails nrx_create with NRX_ERR_INVALID_ARG. */
 int nrx_fused_status(nrx_handle* h, int32_t* status, int32_t reset);
 
-/* Per-handle control of the one-launch forward: enable = 0 the three-launch path; 1 (default)
- * the one-launch forward for the shapes it is measured faster on (U <= 2 with conv1 reading its
- * rows from memory, at least four stages: Var-IO, 8 iterations); 2 for every shape it applies
- * to (also the 2-iteration bench forward, U <= 8 and 2A <= 32 with staged z images; outputs
- * identical to the three launches).  The initial value comes from NRX_FUSED at nrx_create;
- * spin_limit = dependency-wait polls before the timeout error (0: the default, ~0.5 s);
- * inject_err = error bits the next forwards set in the error word (test hook: callers must
- * surface them; 0: none).  Any argument < 0 leaves that setting unchanged. */
+/* Per-handle control of the one-launch forward: enable = 0 no one-launch forward of any kind
+ * (k_forward or k_fwd_col); 1 (default) k_forward only for the shapes it applies to by default
+ * (U <= 2 with conv1 reading its rows from memory, at least four stages) that the column launches
+ * do not take -- no BASELINE shape since round 6; 2 k_forward for every shape it applies to
+ * (also the 2-iteration bench forward, U <= 8 and 2A <= 32 with staged z images; outputs
+ * identical to the launch loop); > 2 invalid.  The initial value comes from NRX_FUSED at
+ * nrx_create; spin_limit = dependency-wait polls before the timeout error (0: the default,
+ * ~0.5 s); inject_err = error bits the next forwards set in the error word (test hook: callers
+ * must surface them; 0: none).  Any argument < 0 leaves that setting unchanged. */
 int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t inject_err);
 
 /* Stage schedule of the three-launch f16 forward, a mask (24-row strip tier):
@@ -335,14 +336,19 @@ int nrx_fused_config(nrx_handle* h, int32_t enable, int32_t spin_limit, int32_t 
  *   bit 3 (8)  the readout update stage as the whole-column launch (k_update_col: 48-position
  *              items, 6 register-resident rows per wave, no halo on grids of <= 48 subcarriers;
  *              taken over bits 0 / 1);
- *   bit 4 (16) StateInit as the whole-column launch (k_init_col: one StateInit, 2A = 8).
+ *   bit 4 (16) StateInit as the whole-column launch (k_init_col: one StateInit, 2A = 8);
+ *   bit 5 (32) the one-launch column forward (k_fwd_col: StateInit + every update in one
+ *              persistent launch, at most one item per CU and stage; opt-in, measured slower);
+ *   bit 6 (64) the column updates on grids wider than one column too (44-output strips;
+ *              measured slower than the RR launch there, so off by default).
  * Each applies where it can -- the update launches with conv1 reading its rows from memory (any
  * U: for U > 2 the combine pass's a_u planes), 2A <= 32, for the readout stage one LLR head
  * whose readout fits -- the strip kernels elsewhere.  0: the strip kernels everywhere; < 0
- * unchanged; > 31 invalid.  Outputs are bit-identical either way.  The initial value comes from
- * NRX_UPDATE_RR (0..31) at nrx_create; the default (29: every column stage, the RR aggregation
- * update where the column one does not apply) is the mask measured fastest.
- * Kernel ids 6 / 7 of nrx_profile_read time the column update / StateInit launches. */
+ * unchanged; > 127 invalid.  Outputs are bit-identical either way.  The initial value comes from
+ * NRX_UPDATE_RR (0..127) at nrx_create; the default (29: column StateInit and column updates on
+ * single-column grids, the RR aggregation update elsewhere) is the mask measured fastest on every
+ * BASELINE shape.  Kernel ids 6 / 7 / 8 of nrx_profile_read time the column
+ * update / StateInit / one-launch column forward. */
 int nrx_update_schedule(nrx_handle* h, int32_t update_rr);
 
 const char* nrx_last_error(void);

@@ -135,7 +135,7 @@ constexpr int kSchedColFwd = 32;   // the one-launch column forward (k_fwd_col) 
 constexpr int kSchedColWide = 64;
 constexpr int kSchedMax = 127;
 // default: the whole-column launches for every stage they apply to, the RR aggregation update
-// where they do not (DESIGN.md section 4; same-box A/B in profiles/r06/)
+// where they do not (DESIGN.md section 5; same-box A/B in profiles/r06/)
 constexpr int kSchedDefault = kSchedColInit | kSchedColAgg | kSchedColRo | kSchedRrAgg;
 constexpr int kFusedSpinLimit = 1 << 21;   // ~0.5 s of s_sleep 4 polls
 

@@ -9,7 +9,7 @@ WB, Var-IO heads, the k_norm pass, the one-launch forward with its U = 4 z image
 combine stages -- are checked
 against the oracle directly, not only for self-consistency.
 
-Tolerances are the ones of tests/test_gpu_parity.py (DESIGN.md section 4):
+Tolerances are the ones of tests/test_gpu_parity.py (DESIGN.md section 6):
 * f32x (f32 storage, f64 arithmetic): LLR max-abs < 1e-3, h_hat max-abs < 1e-4.
 * f16: max-abs <= 10 % of max|LLR|, RMS <= 2 % of RMS(LLR), hard-decision flips
   <= 0.5 % overall and <= 0.1 % where |LLR| > 0.5.

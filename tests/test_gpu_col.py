@@ -110,7 +110,7 @@ def test_col_16_antennas_8_iterations():
 
 def test_col_wide_grid_default_keeps_rr():
     # by default a grid wider than one column runs the column StateInit and the RR aggregation /
-    # strip readout updates (measured faster there: DESIGN.md section 4)
+    # strip readout updates (measured faster there: DESIGN.md section 5)
     case = make_case("nrx_rt", batch=64, users=2, prbs=8, snr_db=12, seed=70)
     ref, _ = _run(case, 0)
     got, pg = _run(case, 29)

@@ -1,4 +1,4 @@
-"""Every BASELINE.json per-GPU shape takes the schedule DESIGN.md section 4 documents as its
+"""Every BASELINE.json per-GPU shape takes the schedule DESIGN.md section 5 documents as its
 default: the per-launch profile of one default forward names the kernels that
 ran each stage.  Random inputs (the schedule depends on shapes only); seeded weights where no
 trained model of that topology exists."""

@@ -1,7 +1,7 @@
 """The one-launch forward (k_forward) against the three-launch forward (needs an MI355X).
 
 k_forward runs the same per-item code as k_init / k_update, only scheduled through per-XCD
-work queues with cross-workgroup dependency counters (DESIGN.md section 11), so its outputs
+work queues with cross-workgroup dependency counters (DESIGN.md section A.11), so its outputs
 must equal the three-launch path bit for bit (``fused_config(enable=False)`` selects that
 path per handle).  The oracle comparison of the same launch shape is tests/test_gpu_baseline_shapes.py
 (cfg2, B = 128, which takes k_forward by default).  Covered here: the bench shape, inactive

@@ -1,4 +1,4 @@
-"""Register-resident update launch (k_update_rr, nrx_rr.inc; DESIGN.md sections 13-14).
+"""Register-resident update launch (k_update_rr, nrx_rr.inc; DESIGN.md sections A.13-A.14).
 
 Every MFMA of k_update_rr sees the operands of the strip kernel's GZ items in the same order, so
 its outputs must equal the strip update kernels' bit for bit: each case runs the three-launch

@@ -1,5 +1,5 @@
 """No inline-asm depthwise result (DPP FMAC) may feed an MFMA, and no VALU result a DPP read, with
-fewer than the 2 wait states gfx940+ requires (tools/hazard_scan.py; DESIGN.md section 14: an
+fewer than the 2 wait states gfx940+ requires (tools/hazard_scan.py; DESIGN.md sections 4.5, A.14: an
 s_waitcnt alone between the two gave the RR kernel wrong B operands; ADVICE r05: one wait state is
 not enough either).  Compiles every kernel translation unit to gfx950 assembly in parallel (~2 min
 on 8 cores) and scans it; skipped where hipcc is absent."""

@@ -5,7 +5,7 @@ writing a VGPR followed by an MFMA reading it with fewer than 2 wait states in b
 LLVM GCNHazardRecognizer's LegacyVALUNotDotWritesVGPRWaitStates = 2).  A hit is a
 pair at distance d <= 2 (d = 1: adjacent, d = 2: one instruction or an s_nop 0 between).  s_nop N
 counts as N + 1 wait states, s_waitcnt as none (measured: an s_waitcnt as the only instruction
-between the two gave wrong MFMA results).  Linear scan per function (labels do not reset the window).
+between the two gave wrong MFMA results, DESIGN.md sections 4.5, A.14).  Linear scan per function (labels do not reset the window).
 
 usage: python tools/hazard_scan.py kernel.s [function-name-substring]
 """
