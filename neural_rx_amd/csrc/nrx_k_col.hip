@@ -48,7 +48,8 @@ hipError_t launch_init_col(const BlockParams<P16>& bp0, hipStream_t st) {
   int items = 0;
   const int grid = col_grid(bp, &items);
   col_stamp_select(st);
-  k_init_col<TAIL_AGG><<<grid, 512, kColLds, st>>>(bp, items);
+  if (items <= grid) k_init_col<TAIL_AGG><<<grid, 512, kColLds, st>>>(bp, items);
+  else k_init_col_multi<TAIL_AGG><<<grid, 512, kColLds, st>>>(bp, items);
   return hipGetLastError();
 }
 
@@ -60,12 +61,24 @@ hipError_t launch_update_col(const BlockParams<P16>& bp0, bool last, hipStream_t
   const int grid = col_grid(bp, &items);
   const bool ch32 = 2 * bp.a.A > 16;
   col_stamp_select(st);
+  // one item per workgroup (the single-column BASELINE shapes) or the looping kernel
+  const bool one = items <= grid;
   if (last) {
-    if (ch32) k_update_col<32, TAIL_READOUT_WB><<<grid, 512, kColLds, st>>>(bp, items);
-    else k_update_col<16, TAIL_READOUT_WB><<<grid, 512, kColLds, st>>>(bp, items);
+    if (ch32) {
+      if (one) k_update_col<32, TAIL_READOUT_WB><<<grid, 512, kColLds, st>>>(bp, items);
+      else k_update_col_multi<32, TAIL_READOUT_WB><<<grid, 512, kColLds, st>>>(bp, items);
+    } else {
+      if (one) k_update_col<16, TAIL_READOUT_WB><<<grid, 512, kColLds, st>>>(bp, items);
+      else k_update_col_multi<16, TAIL_READOUT_WB><<<grid, 512, kColLds, st>>>(bp, items);
+    }
   } else {
-    if (ch32) k_update_col<32, TAIL_AGG><<<grid, 512, kColLds, st>>>(bp, items);
-    else k_update_col<16, TAIL_AGG><<<grid, 512, kColLds, st>>>(bp, items);
+    if (ch32) {
+      if (one) k_update_col<32, TAIL_AGG><<<grid, 512, kColLds, st>>>(bp, items);
+      else k_update_col_multi<32, TAIL_AGG><<<grid, 512, kColLds, st>>>(bp, items);
+    } else {
+      if (one) k_update_col<16, TAIL_AGG><<<grid, 512, kColLds, st>>>(bp, items);
+      else k_update_col_multi<16, TAIL_AGG><<<grid, 512, kColLds, st>>>(bp, items);
+    }
   }
   return hipGetLastError();
 }
@@ -148,10 +161,15 @@ hipError_t setup_col() {
     if (r != hipSuccess) e = r;
   };
   set((const void*)k_init_col<TAIL_AGG>);
+  set((const void*)k_init_col_multi<TAIL_AGG>);
   set((const void*)k_update_col<16, TAIL_AGG>);
   set((const void*)k_update_col<32, TAIL_AGG>);
   set((const void*)k_update_col<16, TAIL_READOUT_WB>);
   set((const void*)k_update_col<32, TAIL_READOUT_WB>);
+  set((const void*)k_update_col_multi<16, TAIL_AGG>);
+  set((const void*)k_update_col_multi<32, TAIL_AGG>);
+  set((const void*)k_update_col_multi<16, TAIL_READOUT_WB>);
+  set((const void*)k_update_col_multi<32, TAIL_READOUT_WB>);
   set((const void*)k_fwd_col<16>);
   return e;
 }
