@@ -50,7 +50,17 @@ L = int(os.environ.get("NRX_STAMP_COL", "-1"))
 print("launch", L, ["StateInit", "aggregation update", "readout update"][L % 3] if L >= 0 else "")
 # m = 5: StateInit: the slot norm is known; UpdateState: the first item's weights are staged
 phases = [("pro", 0, 5), ("conv1", 5, 1), ("exch1", 1, 2), ("conv2", 2, 3), ("exch2", 3, 4), ("conv3+epi", 4, 6)]
-for k in range(4):
+PRO = os.environ.get("NRX_PRO") == "1"
+if PRO:
+    # NRX_PRO_STAMPS build: the first item's prologue and conv1 in the item-1 slots (col_upd_item)
+    chain = [("kernel start", 0, 7), ("item start", 0, 0), ("z rows issued", 1, 0), ("rest weights issued", 1, 1),
+             ("W1 stored", 1, 2), ("barrier", 0, 5), ("step 0 depthwise", 1, 3), ("pass 0 done", 1, 4),
+             ("rest weights stored", 1, 5), ("conv1 done", 0, 1)]
+    ok = (st[:, 0, 6, 0] != 0) & (st[:, 1, 2, 0] != 0)
+    for w in (0, 1):
+        print("   wave", 4 * w, " -> ".join(f"{nm} +{(st[ok, k1, m1, w] - st[ok, k0, m0, w]).mean():.0f}"
+                                       for (_, k0, m0), (nm, k1, m1) in zip(chain, chain[1:])))
+for k in range(1 if PRO else 4):
     s0 = st[:, k, 0, 0]
     if (s0 == 0).all():
         continue
@@ -59,7 +69,7 @@ for k in range(4):
     print(f"item {k}: {ok.sum()} workgroups, item {tot.mean():.0f} cycles (wave 0), min {tot.min()} max {tot.max()}")
     for w in (0, 1):
         print("   wave", 4 * w, "  ".join(f"{nm} {(st[ok, k, b, w] - st[ok, k, a, w]).mean():6.0f}" for nm, a, b in phases))
-for k in range(3):   # the one-launch forward: gap between a workgroup's consecutive items
+for k in range(0 if PRO else 3):   # the one-launch forward: gap between a workgroup's consecutive items
     ok = (st[:, k, 6, 0] != 0) & (st[:, k + 1, 0, 0] != 0)
     if ok.any():
         gap = st[ok, k + 1, 0, 0] - st[ok, k, 6, 0]
