@@ -10,8 +10,8 @@ namespace nrx {
 #include "nrx_col.inc"
 
 bool col_init_applicable(const FwdArgs<_Float16, float, _Float16>& a) {
-  // one StateInit (no Var-IO mix) over 4 rx antennas (2A = A2P = 8: z chunk 0 = [y | h | pe | 0])
-  return a.num_init == 1 && 2 * a.A == 8 && a.init_cinp == 32;
+  // 4 rx antennas (2A = A2P = 8: z chunk 0 = [y | h | pe | 0]); Var-IO: one launch per StateInit m
+  return 2 * a.A == 8 && a.init_cinp == 32;
 }
 
 bool update_col_applicable(const FwdArgs<_Float16, float, _Float16>& a, bool gz, bool last, int sched) {
@@ -48,8 +48,15 @@ hipError_t launch_init_col(const BlockParams<P16>& bp0, hipStream_t st) {
   int items = 0;
   const int grid = col_grid(bp, &items);
   col_stamp_select(st);
-  if (items <= grid) k_init_col<TAIL_AGG><<<grid, 512, kColLds, st>>>(bp, items);
-  else k_init_col_multi<TAIL_AGG><<<grid, 512, kColLds, st>>>(bp, items);
+  // the last StateInit launch runs iteration 0's aggregation MLP (TAIL_AGG), earlier ones (Var-IO) none
+  const bool agg = bp.tail == TAIL_AGG;
+  if (items <= grid) {
+    if (agg) k_init_col<TAIL_AGG><<<grid, 512, kColLds, st>>>(bp, items);
+    else k_init_col<TAIL_NONE><<<grid, 512, kColLds, st>>>(bp, items);
+  } else {
+    if (agg) k_init_col_multi<TAIL_AGG><<<grid, 512, kColLds, st>>>(bp, items);
+    else k_init_col_multi<TAIL_NONE><<<grid, 512, kColLds, st>>>(bp, items);
+  }
   return hipGetLastError();
 }
 
@@ -92,7 +99,8 @@ bool fwd_col_applicable(const FwdArgs<_Float16, float, _Float16>& a, int num_it,
   const int cus = cu_count(), nx = xcc_count();
   if (nx < 1 || nx > 8 || cus % nx != 0) return false;
   const long items = (long)a.B * a.U * col_strips(a.F);
-  return a.U <= kInlineUsers && col_init_applicable(a) && a.ws_bytes < kGzOob && a.pe16 && a.H == 1 &&
+  return a.U <= kInlineUsers && a.num_init == 1 && col_init_applicable(a) && a.ws_bytes < kGzOob && a.pe16 &&
+         a.H == 1 &&
          rr_heads_fit(a.bits_max, 16, 2 * a.A) && items <= cus && num_it >= 1 && 1 + num_it <= kColMaxStages &&
          a.B <= kFusedMaxB;
 }
@@ -161,7 +169,9 @@ hipError_t setup_col() {
     if (r != hipSuccess) e = r;
   };
   set((const void*)k_init_col<TAIL_AGG>);
+  set((const void*)k_init_col<TAIL_NONE>);
   set((const void*)k_init_col_multi<TAIL_AGG>);
+  set((const void*)k_init_col_multi<TAIL_NONE>);
   set((const void*)k_update_col<16, TAIL_AGG>);
   set((const void*)k_update_col<32, TAIL_AGG>);
   set((const void*)k_update_col<16, TAIL_READOUT_WB>);

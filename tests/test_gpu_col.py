@@ -119,15 +119,32 @@ def test_col_wide_grid_default_keeps_rr():
 
 
 def test_col_var_io():
-    # Var-IO (two StateInits: the strip k_init), one-hot MCS mask; the aggregation update runs the
-    # column launch, the readout (two LLR heads) the strip kernel
+    # Var-IO (two StateInits: two column StateInit launches, the second accumulating; the profiler
+    # times the stage as one event pair), one-hot MCS mask; the aggregation update runs the column
+    # launch, the readout (two LLR heads) the strip kernel
     rng = np.random.default_rng(79)
     case = make_case("nrx_rt_var_mcs", batch=128, users=2, prbs=4, snr_db=14, seed=79,
                      mcs_choice=rng.integers(0, 2, size=(128, 2)))
     n_it = case.spec.num_it
     ref, _ = _run(case, 0)
     got, pg = _run(case, COL)
-    assert pg["state_init_col"][0] == 0 and pg["state_update_col"][0] == n_it - 1, pg
+    assert pg["state_init_col"][0] == 1 and pg["state_init"][0] == 0, pg
+    assert pg["state_update_col"][0] == n_it - 1, pg
+    assert np.array_equal(ref["llr_raw"], got["llr_raw"])
+    assert np.array_equal(ref["h_hat"], got["h_hat"])
+    c = compare(run_oracle(case), got)
+    assert c["llr_rel"] < 0.10 and c["llr_rms_rel"] < 0.02 and c["flip_rate_confident"] <= 1e-3, c
+
+
+def test_col_var_io_one_mcs_everywhere():
+    # every (slot, user) on MCS 1: StateInit 0's launch has weight 0 everywhere (its items' output
+    # enters as 0 * finite), StateInit 1's launch adds the whole state
+    # (B = 128, 4 PRB: more items than the small-strip latency tiers take)
+    case = make_case("nrx_rt_var_mcs", batch=128, users=2, prbs=4, snr_db=14, seed=81,
+                     mcs_choice=np.ones((128, 2), np.int64))
+    ref, _ = _run(case, 0)
+    got, pg = _run(case, COL)
+    assert pg["state_init_col"][0] == 1, pg
     assert np.array_equal(ref["llr_raw"], got["llr_raw"])
     assert np.array_equal(ref["h_hat"], got["h_hat"])
 

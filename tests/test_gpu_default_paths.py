@@ -48,14 +48,14 @@ def test_cfg3_rr_updates_on_a_wide_grid():
 
 
 def test_cfg4_var_io():
-    # Var-IO (two StateInits), 2 UE, 4 PRB, 128 slots: strip StateInits, the column aggregation
-    # update, the strip readout (two LLR heads)
+    # Var-IO (two StateInits), 2 UE, 4 PRB, 128 slots: two column StateInit launches, the column
+    # aggregation update, the strip readout (two LLR heads)
     rng = np.random.default_rng(4)
     case = make_case("nrx_rt_var_mcs", batch=128, users=2, prbs=4, random_inputs=True, seed=4,
                      mcs_choice=rng.integers(0, 2, size=(128, 2)))
     prof = _profile(case)
     # (the profiler times the StateInit stage's two launches as one event pair)
-    assert prof == {"state_init": 1, "state_update_col": 1, "state_update": 1}, prof
+    assert prof == {"state_init_col": 1, "state_update_col": 1, "state_update": 1}, prof
 
 
 def test_cfg4p_masking_8_iterations():
