@@ -431,12 +431,23 @@ static int forward_slots(nrx_handle* h, const nrx_io* io, int llr_B, void* works
 // the previous one-launch forward's while that forward has not finished (the counters are per
 // handle).  Called before ANY launch of a forward entry point, so a refused call has launched
 // nothing (the y-layout / Aerial preprocessing used to run first).
+static int chunk_slots(const nrx_shape* s, int precision);
+
 static int fused_busy(nrx_handle* h, const nrx_io* io, hipStream_t st, bool* takes) {
   *takes = false;
   if (io->precision != NRX_PREC_F16) return NRX_OK;
-  FwdArgs<_Float16, float, _Float16> a{};
-  fill_args(a, h, io, nullptr, h->m16.init_cinp);   // pointers unused: the decision needs sizes only
-  *takes = fused_would_run(a, io->num_it, h->fused_ctl());
+  // decided on the shapes the forward will run: a forward above the 1 GB workspace runs as slot
+  // chunks (nrx_forward), full ones of chunk_slots slots and a remainder, and each chunk may take
+  // the one-launch path although the whole batch would not
+  const int B = io->shape.batch, bc = chunk_slots(&io->shape, io->precision);
+  for (const int n : {bc < B ? bc : B, bc < B && B % bc ? B % bc : 0}) {
+    if (n <= 0) continue;
+    nrx_io c = *io;
+    c.shape.batch = n;
+    FwdArgs<_Float16, float, _Float16> a{};
+    fill_args(a, h, &c, nullptr, h->m16.init_cinp);   // pointers unused: the decision needs sizes only
+    *takes = *takes || fused_would_run(a, io->num_it, h->fused_ctl());
+  }
   if (*takes && h->have_last && h->last_stream != st && hipEventQuery(h->last_ev) == hipErrorNotReady)
     return fail(NRX_ERR_BUSY, "a one-launch forward of this handle is still running on another stream");
   return NRX_OK;

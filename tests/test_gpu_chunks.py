@@ -52,3 +52,23 @@ def test_chunked_forward_eight_users_combine_pass():
         eng.close()
     assert np.array_equal(full["llr_raw"], np.concatenate([lo["llr_raw"], hi["llr_raw"]], axis=1))
     assert np.array_equal(full["h_hat"], np.concatenate([lo["h_hat"], hi["h_hat"]], axis=0))
+
+
+def test_chunked_forward_multi_head():
+    # Var-IO (two LLR heads: the LLR tensor keeps its head stride llr_B across chunks):
+    # 26 slots at 273 PRB run as chunks and must equal forwards of 13 + 13 slots for every head
+    from neural_rx_amd.receiver import CGNNEngine
+    rng = np.random.default_rng(63)
+    case = make_case("nrx_rt_var_mcs", batch=26, users=2, prbs=273, random_inputs=True, seed=63,
+                     mcs_choice=rng.integers(0, 2, size=(26, 2)))
+    eng = CGNNEngine(case.spec, case.weights)
+    try:
+        assert eng.workspace_bytes(26, 2, 3276) < (1 << 30)
+        full = run_engine(case, "f16", eng)
+        lo = run_engine(_sub(case, 0, 13), "f16", eng)
+        hi = run_engine(_sub(case, 13, 26), "f16", eng)
+    finally:
+        eng.close()
+    assert full["llr_raw"].shape[0] == 2
+    assert np.array_equal(full["llr_raw"], np.concatenate([lo["llr_raw"], hi["llr_raw"]], axis=1))
+    assert np.array_equal(full["h_hat"], np.concatenate([lo["h_hat"], hi["h_hat"]], axis=0))
